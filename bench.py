@@ -1,0 +1,211 @@
+"""Throughput of the MI355X Sep-TFAnet^VAD forward path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one ``SeparationModel.forward`` (config_with_vad.json) over a resident batch of 64
+synthetic 2-speaker mixtures of 32 000 samples (4 s @ 8 kHz resampled to 16 kHz by the
+reference's CLI, only_inference.py:76-79 => T = 126 frames) per GPU. For N > 1 the driver launches
+one process per GPU (torchrun); every rank runs its own shard of utterances (weak scaling, no
+collective on the data path, only barriers around the timed region). Rank 0 prints one JSON line.
+
+Extra fields:
+  roofline      dominant kernel = DepthConv1d.res_out GEMM (512->256, fp32 MFMA); algorithmic FLOPs
+                per launch / its average launch time, from HIP events recorded by libsepvad on the
+                stream the kernels run on, during the timed steps.
+  cpu_baseline  the oracle CPU restatement (oracle/torch_ref.py, torch fp32) on the host cores,
+                rank 0 at N=1 only, on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "utterances/sec/GPU (4s@8kHz, 2spk+VAD); SI-SDR within 0.01 dB of ref"
+B_PER_GPU = 64
+N_SAMPLES = 32000
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix (= vector) peak, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def gemm_flops_per_utt(T):
+    """Algorithmic FLOPs of the 1x1 GEMMs per utterance: 9 700 352 * T."""
+    return (24 * (2 * 256 * 256 + 2 * 512 * 256) + 2 * 514 * 256) * T
+
+
+def res_out_flops(B, T):
+    return 2 * 256 * 512 * B * T
+
+
+def cpu_baseline(seconds: float = 12.0):
+    """Oracle (CPU restatement, torch fp32) on the host: batches of the same workload until
+    `seconds` of CPU work have elapsed (at least 2 batches)."""
+    from oracle.torch_ref import OracleModel
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(threads)
+    sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234).items()}
+    om = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float32)
+    x, _ = synth.make_batch(B_PER_GPU, N_SAMPLES, 7000)
+    xt = torch.from_numpy(x)
+    om(xt[:2])  # warm-up
+    n_utt, t0 = 0, time.perf_counter()
+    while True:
+        om(xt)
+        n_utt += B_PER_GPU
+        el = time.perf_counter() - t0
+        if el >= seconds and n_utt >= 2 * B_PER_GPU:
+            break
+    return dict(value=n_utt / el, unit="utterances/s", cores=threads, kind="port",
+                sample=f"{n_utt} utterances ({n_utt // B_PER_GPU} batches of B={B_PER_GPU}, N={N_SAMPLES}) "
+                       f"in {el:.1f} s, oracle/torch_ref.py fp32 on {threads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=B_PER_GPU, help="utterances per GPU per step")
+    ap.add_argument("--samples", type=int, default=N_SAMPLES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    cfg = pkg.CONFIG_WITH_VAD
+    net = pkg.SeparationModel(**cfg) if rank == 0 else None
+    if net is None:
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO()):
+            net = pkg.SeparationModel(**cfg)
+    sd = synth.make_state_dict(cfg, 1234)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net = net.eval().to(dev)
+    B, N = args.batch, args.samples
+    T = 1 + N // 256
+    # this rank's shard of utterances: global utterance ids [rank*B, (rank+1)*B)
+    x, _ = synth.make_batch(B, N, 10_000 + rank * B)
+    x = torch.from_numpy(x).to(dev)
+    h = net.native_handle(dev)
+    h.reserve(B, N)
+
+    def step():
+        with torch.no_grad():
+            return net(x)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # timed region (value)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # per-kernel timing pass (HIP events on the kernels' stream), same steps
+    h.set_timing(True)
+    gemm_ms = res_ms = tot_ms = 0.0
+    n_res = n_gemm = 0
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+        tm = h.timing()
+        gemm_ms += tm["gemm_ms"]; res_ms += tm["res_out_ms"]; tot_ms += tm["total_ms"]
+        n_res += tm["res_out_launches"]; n_gemm += tm["gemm_launches"]
+    h.set_timing(False)
+    torch.cuda.synchronize()
+
+    if rank == 0:
+        total_utt = world * B * args.steps
+        value = total_utt / el
+        res_avg_s = res_ms / n_res / 1e3
+        achieved = res_out_flops(B, T) / res_avg_s / 1e12
+        fwd_timed = n_gemm / (2 * 24 + 1)  # 49 GEMM launches per forward
+        all_gemm_tflops = gemm_flops_per_utt(T) * B * fwd_timed / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "r01_pmc_res_out.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "utterances/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
+                    "recipe weights (pretrained .pth absent from the reference)",
+            "config": {
+                "workload": f"cfg2 config_with_vad.json forward, B={B}/GPU, N={N} samples (4 s @ 8 kHz resampled "
+                            f"to 16 kHz), T={T} frames; full forward incl. STFT, 24 TCN blocks, VAD, iSTFT and "
+                            f"the reference's side outputs",
+                "global_batch": world * B,
+                "seq_len": N,
+                "parallelism": f"dp{world} (independent utterance shards, no data-path collective)",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "k_pw_gemm<LD_GN,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, fp32 MFMA 32x32x2)",
+                "achieved": round(achieved, 3),
+                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "flops_per_launch": res_out_flops(B, T),
+                "avg_launch_us": round(res_avg_s * 1e6, 2),
+                "all_gemms_tflops": round(all_gemm_tflops, 3) if all_gemm_tflops else None,
+                "gemm_share_of_forward": round(gemm_ms / tot_ms, 3) if tot_ms > 0 else None,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

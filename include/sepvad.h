@@ -1,0 +1,119 @@
+/*
+ * sepvad.h — C ABI of libsepvad.so, the MI355X (gfx950) Sep-TFAnet^VAD forward path.
+ *
+ * The reference has no native interface: its hot path is the PyTorch module
+ * `SeparationModel` (reference model/model.py:360-461) called as
+ *     model = SeparationModel(**config["arch"]["args"])      (parse_config.py:99-103)
+ *     model.load_state_dict(ckpt["state_dict"], strict=True)  (only_inference.py:57-61)
+ *     sep, vad, est = model(x, inference_kw)                  (only_inference.py:90-91,
+ *                                                               model/online_class_unknown_targets.py:84)
+ * Each entry point below replaces one of those steps; the Python host
+ * (sep-tfanet-vad_amd/model.py, native.py) binds them with ctypes. Plain pointers and sizes
+ * only; no torch types cross this boundary. All device pointers are HIP device memory on
+ * the handle's device; calls are ordered on the caller's hipStream_t.
+ *
+ * Errors: functions return SEPVAD_OK (0) or a negative status; sepvad_last_error() gives a
+ * thread-local message. The Python host turns a non-zero status into RuntimeError.
+ */
+#ifndef SEPVAD_H
+#define SEPVAD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEPVAD_ABI_VERSION 1
+
+enum {
+  SEPVAD_OK = 0,
+  SEPVAD_E_ARG = -1,      /* invalid argument / unsupported configuration */
+  SEPVAD_E_WEIGHTS = -2,  /* missing or mis-shaped state_dict entry */
+  SEPVAD_E_HIP = -3,      /* a HIP runtime call failed */
+  SEPVAD_E_SHAPE = -4     /* B/N outside what the handle supports */
+};
+
+/* TCN residual mode (model/model.py:347-352). */
+enum { SEPVAD_LN_PLAIN = 0, SEPVAD_LN_RECURSIVE = 1, SEPVAD_LN_RESIDUAL = 2 };
+
+/* Arithmetic of the pointwise (1x1) GEMMs. FP32 is the parity path (max-abs <= 1e-4). */
+enum { SEPVAD_PREC_FP32 = 0 };
+
+/* SeparationModel kwargs that change the computation (model/model.py:362-366). */
+typedef struct SepVadConfig {
+  int32_t n_fft;                      /* n_fftBins; 512 */
+  int32_t bn_dim;                     /* BN_dim; must be n_fft/2 */
+  int32_t h_dim;                      /* H_dim; must be 2*bn_dim */
+  int32_t layer;                      /* blocks per stack */
+  int32_t stack;                      /* stacks; blocks = layer*stack */
+  int32_t num_spk;                    /* 2 */
+  int32_t tf_attention;               /* TF_Attention after every block */
+  int32_t ln_mode;                    /* SEPVAD_LN_* */
+  int32_t final_vad;                  /* VAD head present */
+  int32_t final_vad_masked_speakers;  /* VAD on masked magnitudes instead of pre-sigmoid masks */
+  int32_t noisy_phase;                /* est = (|X| m) e^{j angle X} instead of X m */
+  int32_t activity_input;             /* 3x3 activity gate on the dB spectrum */
+  int32_t precision;                  /* SEPVAD_PREC_* */
+} SepVadConfig;
+
+/* forward()'s inference_kw (only_inference.py:102-108; model/model.py:444-457). */
+typedef struct SepVadInferKw {
+  int32_t enabled;                    /* 0 == empty dict: the branch is skipped */
+  int32_t filter_signals_by_smo_vad;
+  int32_t filter_signals_by_unsmo_vad;
+  int32_t length_smoothing_filter;    /* accepted, no effect on the math (reference overrides the taps) */
+  float threshold_activated_vad;
+  int32_t return_smoothed_vad;
+} SepVadInferKw;
+
+/* Caller-owned outputs of one forward (device pointers). T = 1 + N / (n_fft/2). */
+typedef struct SepVadOutputs {
+  float* sep;       /* [B, num_spk, N] f32, required                                        */
+  float* vad;       /* [B, num_spk, T] f32 (probabilities, or {0,1} when smoothed); NULL if !final_vad */
+  void* est;        /* [B, num_spk, n_fft/2+1, T] complex64 (re,im interleaved); nullable  */
+  float* spectrum;  /* [B, n_fft/2+1, T] gated dB spectrum (self.spectrum); nullable         */
+  float* masks_b;   /* [B, num_spk*(n_fft/2+1), T] pre-sigmoid masks (self.masks_b); nullable */
+  float* mask;      /* [B, num_spk, n_fft/2+1, T] post-sigmoid (self.mask_per_speaker); nullable */
+} SepVadOutputs;
+
+typedef struct sepvad_model* sepvad_handle;
+
+/* Replaces SeparationModel(**args) + load_state_dict(strict=True) (model/model.py:361-400,
+ * only_inference.py:57-61). `tensors[i]` is a HOST float32 array of `numels[i]` elements named
+ * `names[i]` (reference state_dict keys). Folds weight-norm (w = v * (g/||v||)) once, packs the
+ * weights for the kernels and uploads them to `device`. Returns NULL on error. */
+sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors,
+                            const char* const* names, const int64_t* numels, int32_t n,
+                            int32_t device);
+
+/* Pre-size the workspace for up to B utterances of N samples (so forward never allocates). */
+int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N);
+
+/* Replaces SeparationModel.forward(x, inference_kw) (model/model.py:402-461).
+ * x: device [B, N] f32. kw may be NULL (== empty dict). Stream-ordered on `stream`
+ * (a hipStream_t; NULL = default stream). */
+int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N,
+                       const SepVadOutputs* out, const SepVadInferKw* kw, void* stream);
+
+/* Front-end / back-end stages alone, for kernel-level parity tests:
+ * STFT with DC zeroed (model/model.py:16-25,408-410) -> X [B, n_fft/2+1, T] complex64, and
+ * 10 log10(clamp(|X|^2, 1e-10)) (model/model.py:411-412) -> spec [B, n_fft/2+1, T] (nullable). */
+int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec,
+                    void* stream);
+/* torch.istft(center=True, length=N) of est [B*S, n_fft/2+1, T] complex64 (model/model.py:460). */
+int32_t sepvad_istft(sepvad_handle h, const void* est, int32_t BS, int32_t N, float* y, void* stream);
+
+/* Seconds of the last forward's dominant-kernel launches measured with HIP events
+ * (enabled by sepvad_set_timing(h, 1)); see bench.py. */
+int32_t sepvad_set_timing(sepvad_handle h, int32_t on);
+int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, double* total_ms);
+
+void sepvad_destroy(sepvad_handle h);
+const char* sepvad_last_error(void);
+int32_t sepvad_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEPVAD_H */

@@ -1,0 +1,581 @@
+// C ABI of libsepvad.so (include/sepvad.h): weight folding/packing at create time and the
+// stream-ordered launch sequence of one SeparationModel.forward (reference model/model.py:402-461).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/sepvad.h"
+#include "sepvad_internal.h"
+
+using namespace sepvad;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(SEPVAD_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
+  } while (0)
+
+struct BlockOff {
+  size_t w1t, b1, g1, be1, wd, bd, w2t, b2, g2, be2, attp, lna_g, lna_b, lnb_g, lnb_b;
+  float a1, a2;
+  int dil;
+};
+
+struct Workspace {
+  int Bmax = 0, Tpmax = 0;
+  char* base = nullptr;
+  size_t bytes = 0;
+  float2* X; float* specdb; float* S0; float* O[2]; float* A; float* D; float* R; float* U;
+  float* P; float* masks; float* gain; float* colsum; float* rowsum; float* vad;
+  double* sl_gate; double* sl_g1; double* sl_dw; double* sl_att; double* sl_hp; double* moments;
+};
+
+}  // namespace
+
+struct sepvad_model {
+  SepVadConfig cfg{};
+  int device = 0;
+  int nblk = 0;
+  float* dparams = nullptr;  // packed weights (device)
+  std::vector<BlockOff> blk;
+  size_t win_in = 0, win_out = 0, win_inv = 0, tw = 0;
+  size_t ln_g = 0, ln_b = 0;
+  size_t out_g = 0, out_b = 0, wot = 0, bo = 0;
+  float out_a = 0.f;
+  size_t v_w1 = 0, v_b1 = 0, v_g = 0, v_b = 0, v_w2 = 0;
+  float v_a = 0.f, v_b2 = 0.f;
+  size_t gate = 0;
+  bool same_stft_window = true;
+  Workspace ws;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  double gemm_ms = 0.0, g2_ms = 0.0, total_ms = 0.0;
+  int gemm_launches = 0, g2_launches = 0;
+
+  const float* P(size_t off) const { return dparams + off; }
+};
+
+namespace {
+
+struct TensorMap {
+  std::unordered_map<std::string, std::pair<const float*, int64_t>> m;
+  const float* get(const std::string& k, int64_t numel) const {
+    auto it = m.find(k);
+    if (it == m.end()) { g_err = "missing state_dict entry: " + k; return nullptr; }
+    if (it->second.second != numel) {
+      g_err = "state_dict entry " + k + " has " + std::to_string(it->second.second) +
+              " elements, expected " + std::to_string(numel);
+      return nullptr;
+    }
+    return it->second.first;
+  }
+};
+
+struct Packer {
+  std::vector<float> blob;
+  size_t add(const float* p, size_t n) {
+    size_t off = blob.size();
+    // keep every array 16-byte aligned for float4 loads
+    blob.insert(blob.end(), p, p + n);
+    while (blob.size() % 4) blob.push_back(0.f);
+    return off;
+  }
+  size_t add(const std::vector<float>& v) { return add(v.data(), v.size()); }
+};
+
+// torch.nn.utils.weight_norm (dim=0): w = v * (g / ||v||_2 over all dims but 0).
+std::vector<float> fold_wn(const float* g, const float* v, int cout, int rest) {
+  std::vector<float> w((size_t)cout * rest);
+  for (int o = 0; o < cout; ++o) {
+    double s = 0.0;
+    for (int i = 0; i < rest; ++i) s += (double)v[(size_t)o * rest + i] * v[(size_t)o * rest + i];
+    const float nrm = (float)std::sqrt(s);
+    const float scale = g[o] / nrm;
+    for (int i = 0; i < rest; ++i) w[(size_t)o * rest + i] = v[(size_t)o * rest + i] * scale;
+  }
+  return w;
+}
+
+// [cout][cin] -> [cin][mpad] (k-major, zero-padded columns)
+std::vector<float> transpose_pad(const std::vector<float>& w, int cout, int cin, int mpad) {
+  std::vector<float> t((size_t)cin * mpad, 0.f);
+  for (int o = 0; o < cout; ++o)
+    for (int i = 0; i < cin; ++i) t[(size_t)i * mpad + o] = w[(size_t)o * cin + i];
+  return t;
+}
+
+int ws_reserve(sepvad_model* h, int B, int N) {
+  const int T = 1 + N / HOP;
+  const int Tp = round_up(T, TILE);
+  if (B <= h->ws.Bmax && Tp <= h->ws.Tpmax) return SEPVAD_OK;
+  const int Bm = std::max(B, h->ws.Bmax), Tm = std::max(Tp, h->ws.Tpmax);
+  if (h->ws.base) { (void)hipFree(h->ws.base); h->ws.base = nullptr; }
+  const size_t bt = (size_t)Bm * Tm;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
+  const size_t oX = take(bt * NBIN * 8), oSpec = take(bt * NBIN * 4), oS0 = take(bt * CH * 4);
+  const size_t oO0 = take(bt * CH * 4), oO1 = take(bt * CH * 4), oA = take(bt * CH * 4);
+  const size_t oD = take(bt * HID * 4), oR = take(bt * CH * 4), oU = take(bt * CH * 4);
+  const size_t oP = take(bt * CH * 4), oM = take(bt * 2 * NBIN * 4), oG = take(bt * 2 * 4);
+  const size_t oCs = take(bt * (CH / TILE) * 4), oRs = take((size_t)Bm * (Tm / TILE) * CH * 4);
+  const size_t oV = take(bt * 2 * 4);
+  const size_t oSg = take((size_t)Bm * gate_tiles() * 16), oS1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
+  const size_t oSd = take((size_t)Bm * 16 * 16), oSa = take((size_t)Bm * 16 * 16), oSh = take((size_t)Bm * 16 * 16);
+  const size_t oMo = take((size_t)Bm * CH * 5 * 8);
+  char* base = nullptr;
+  HIPCHK(hipMalloc(&base, off));
+  HIPCHK(hipMemset(base, 0, off));
+  Workspace& w = h->ws;
+  w.base = base; w.bytes = off; w.Bmax = Bm; w.Tpmax = Tm;
+  w.X = (float2*)(base + oX); w.specdb = (float*)(base + oSpec); w.S0 = (float*)(base + oS0);
+  w.O[0] = (float*)(base + oO0); w.O[1] = (float*)(base + oO1); w.A = (float*)(base + oA);
+  w.D = (float*)(base + oD); w.R = (float*)(base + oR); w.U = (float*)(base + oU);
+  w.P = (float*)(base + oP); w.masks = (float*)(base + oM); w.gain = (float*)(base + oG);
+  w.colsum = (float*)(base + oCs); w.rowsum = (float*)(base + oRs); w.vad = (float*)(base + oV);
+  w.sl_gate = (double*)(base + oSg); w.sl_g1 = (double*)(base + oS1); w.sl_dw = (double*)(base + oSd);
+  w.sl_att = (double*)(base + oSa); w.sl_hp = (double*)(base + oSh); w.moments = (double*)(base + oMo);
+  return SEPVAD_OK;
+}
+
+// The loader transform that turns (o_{i}, u_{i}) of block i into the next block input o_{i+1}.
+LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float* U) {
+  LoadSpec ld{};
+  ld.X = O; ld.X2 = U;
+  const BlockOff& bo = h->blk[i];
+  if (h->cfg.ln_mode == SEPVAD_LN_RECURSIVE) {
+    ld.mode = LD_RECURSIVE;
+    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
+    ld.g2 = h->P(bo.lnb_g); ld.be2 = h->P(bo.lnb_b); ld.eps2 = 1e-5f;
+    ld.moments = h->ws.moments;
+  } else if (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL) {
+    ld.mode = LD_RESIDUAL;
+    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
+    ld.slots = h->ws.sl_att; ld.nslots = CH / 16;
+  } else {
+    ld.mode = LD_ADD;
+  }
+  return ld;
+}
+
+
+// Restores the caller's current HIP device on scope exit (torch shares this runtime).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int ev_record(sepvad_model* h, hipStream_t s) {
+  if (!h->timing) return 0;
+  hipEvent_t e;
+  HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(e, s));
+  h->ev.push_back(e);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sepvad_last_error(void) { return g_err.c_str(); }
+int32_t sepvad_abi_version(void) { return SEPVAD_ABI_VERSION; }
+
+sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors, const char* const* names,
+                            const int64_t* numels, int32_t n, int32_t device) {
+  if (!cfg || !tensors || !names || !numels) { g_err = "null argument"; return nullptr; }
+  const SepVadConfig& c = *cfg;
+  if (c.n_fft != NFFT || c.bn_dim != CH || c.h_dim != HID || c.num_spk != 2 || c.precision != SEPVAD_PREC_FP32 ||
+      c.layer < 1 || c.stack < 1) {
+    g_err = "unsupported configuration (native path: n_fft=512, BN_dim=256, H_dim=512, num_spk=2, fp32)";
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) { g_err = "invalid device"; return nullptr; }
+  DeviceGuard dg(device);
+  TensorMap tm;
+  for (int i = 0; i < n; ++i) tm.m[names[i]] = {tensors[i], numels[i]};
+  auto* h = new sepvad_model();
+  h->cfg = c;
+  h->device = device;
+  h->nblk = c.layer * c.stack;
+  Packer pk;
+  bool ok = true;
+  auto get = [&](const std::string& k, int64_t numel) -> const float* {
+    const float* p = tm.get(k, numel);
+    if (!p) ok = false;
+    return p;
+  };
+  // windows (model/model.py:383-387) and FFT twiddles
+  const float* wi = get("spec_input.spec.window", NFFT);
+  const float* wo = get("spec_output.window", NFFT);
+  const float* wv = get("inv_spec.window", NFFT);
+  if (!ok) { delete h; return nullptr; }
+  h->win_in = pk.add(wi, NFFT);
+  h->win_out = pk.add(wo, NFFT);
+  h->win_inv = pk.add(wv, NFFT);
+  h->same_stft_window = std::memcmp(wi, wo, NFFT * sizeof(float)) == 0;
+  {
+    std::vector<float> tw(2 * NFFT);
+    for (int m = 0; m < NFFT; ++m) {
+      const double ang = -2.0 * M_PI * m / NFFT;
+      tw[2 * m] = (float)std::cos(ang);
+      tw[2 * m + 1] = (float)std::sin(ang);
+    }
+    h->tw = pk.add(tw);
+  }
+  h->ln_g = pk.add(get("TCN.LN.weight", CH), CH);
+  h->ln_b = pk.add(get("TCN.LN.bias", CH), CH);
+  if (!ok) { delete h; return nullptr; }
+  // blocks (model/model.py:285-295,103-127,182-195,310-319)
+  for (int i = 0; i < h->nblk; ++i) {
+    BlockOff bo{};
+    const std::string p = "TCN.TCN." + std::to_string(i);
+    const float* g1 = get(p + ".conv1d.weight_g", CH);
+    const float* v1 = get(p + ".conv1d.weight_v", (int64_t)CH * CH);
+    const float* gd = get(p + ".dconv1d.weight_g", HID);
+    const float* vd = get(p + ".dconv1d.weight_v", (int64_t)HID * 3);
+    const float* g2 = get(p + ".res_out.weight_g", CH);
+    const float* v2 = get(p + ".res_out.weight_v", (int64_t)CH * HID);
+    const float* b1 = get(p + ".conv1d.bias", CH);
+    const float* bd = get(p + ".dconv1d.bias", HID);
+    const float* b2 = get(p + ".res_out.bias", CH);
+    const float* a1 = get(p + ".nonlinearity1.weight", 1);
+    const float* a2 = get(p + ".nonlinearity2.weight", 1);
+    const float* r1g = get(p + ".reg1.weight", CH);
+    const float* r1b = get(p + ".reg1.bias", CH);
+    const float* r2g = get(p + ".reg2.weight", HID);
+    const float* r2b = get(p + ".reg2.bias", HID);
+    if (!ok) { delete h; return nullptr; }
+    bo.w1t = pk.add(transpose_pad(fold_wn(g1, v1, CH, CH), CH, CH, CH));
+    bo.b1 = pk.add(b1, CH);
+    bo.g1 = pk.add(r1g, CH);
+    bo.be1 = pk.add(r1b, CH);
+    bo.wd = pk.add(fold_wn(gd, vd, HID, 3));
+    bo.bd = pk.add(bd, HID);
+    bo.w2t = pk.add(transpose_pad(fold_wn(g2, v2, CH, HID), CH, HID, CH));
+    bo.b2 = pk.add(b2, CH);
+    bo.g2 = pk.add(r2g, HID);
+    bo.be2 = pk.add(r2b, HID);
+    bo.a1 = a1[0];
+    bo.a2 = a2[0];
+    const int li = i % c.layer;
+    bo.dil = li == 0 ? 1 : (li % 4 + 1);
+    std::vector<float> attp(20, 0.f);
+    if (c.tf_attention) {
+      const std::string q = "TCN.time_freq_attnetion." + std::to_string(i);
+      const char* convs[4] = {".conv1d_t_1", ".conv1d_t_2", ".conv1d_f_1", ".conv1d_f_2"};
+      for (int j = 0; j < 4; ++j) {
+        const float* w = get(q + convs[j] + ".weight", 3);
+        const float* bb = get(q + convs[j] + ".bias", 1);
+        if (!ok) { delete h; return nullptr; }
+        attp[4 * j + 0] = w[0]; attp[4 * j + 1] = w[1]; attp[4 * j + 2] = w[2]; attp[4 * j + 3] = bb[0];
+      }
+      const float* pt = get(q + ".prelu_t.weight", 1);
+      const float* pf = get(q + ".prelu_f.weight", 1);
+      if (!ok) { delete h; return nullptr; }
+      attp[16] = pt[0]; attp[17] = pf[0];
+    }
+    bo.attp = pk.add(attp);
+    if (c.ln_mode == SEPVAD_LN_RECURSIVE) {
+      bo.lna_g = pk.add(get("TCN.ln_first_modules." + std::to_string(i) + ".weight", CH), CH);
+      bo.lna_b = pk.add(get("TCN.ln_first_modules." + std::to_string(i) + ".bias", CH), CH);
+      bo.lnb_g = pk.add(get("TCN.ln_second_modules." + std::to_string(i) + ".weight", CH), CH);
+      bo.lnb_b = pk.add(get("TCN.ln_second_modules." + std::to_string(i) + ".bias", CH), CH);
+    } else if (c.ln_mode == SEPVAD_LN_RESIDUAL) {
+      bo.lna_g = pk.add(get("TCN.ln_modules." + std::to_string(i) + ".weight", CH), CH);
+      bo.lna_b = pk.add(get("TCN.ln_modules." + std::to_string(i) + ".bias", CH), CH);
+    }
+    if (!ok) { delete h; return nullptr; }
+    h->blk.push_back(bo);
+  }
+  // output head (model/model.py:322-325)
+  {
+    const float* oa = get("TCN.output.0.weight", 1);
+    const float* og = get("TCN.output.1.weight", CH);
+    const float* ob = get("TCN.output.1.bias", CH);
+    const float* gg = get("TCN.output.2.weight_g", 2 * NBIN);
+    const float* vv = get("TCN.output.2.weight_v", (int64_t)2 * NBIN * CH);
+    const float* bb = get("TCN.output.2.bias", 2 * NBIN);
+    if (!ok) { delete h; return nullptr; }
+    h->out_a = oa[0];
+    h->out_g = pk.add(og, CH);
+    h->out_b = pk.add(ob, CH);
+    h->wot = pk.add(transpose_pad(fold_wn(gg, vv, 2 * NBIN, CH), 2 * NBIN, CH, MOUT_PAD));
+    std::vector<float> bpad(MOUT_PAD, 0.f);
+    std::memcpy(bpad.data(), bb, 2 * NBIN * sizeof(float));
+    h->bo = pk.add(bpad);
+  }
+  // VAD head (model/model.py:153-171)
+  if (c.final_vad) {
+    const float* g1 = get("vad.common.conv1_1.weight_g", 4);
+    const float* v1 = get("vad.common.conv1_1.weight_v", (int64_t)4 * NBIN * 5);
+    const float* b1 = get("vad.common.conv1_1.bias", 4);
+    const float* a = get("vad.common.relu_1.weight", 1);
+    const float* gg = get("vad.common.BN_1.weight", 4);
+    const float* gb = get("vad.common.BN_1.bias", 4);
+    const float* g2 = get("vad.output_layer_vad.weight_g", 1);
+    const float* v2 = get("vad.output_layer_vad.weight_v", 12);
+    const float* b2 = get("vad.output_layer_vad.bias", 1);
+    if (!ok) { delete h; return nullptr; }
+    h->v_w1 = pk.add(fold_wn(g1, v1, 4, NBIN * 5));
+    h->v_b1 = pk.add(b1, 4);
+    h->v_a = a[0];
+    h->v_g = pk.add(gg, 4);
+    h->v_b = pk.add(gb, 4);
+    h->v_w2 = pk.add(fold_wn(g2, v2, 1, 12));
+    h->v_b2 = b2[0];
+  }
+  // activity gate (model/model.py:398-400)
+  {
+    std::vector<float> gw(12, 0.f);
+    if (c.activity_input) {
+      const float* w = get("activity_input.weight", 9);
+      const float* bb = get("activity_input.bias", 1);
+      const float* pa = get("prelu.weight", 1);
+      if (!ok) { delete h; return nullptr; }
+      std::memcpy(gw.data(), w, 9 * sizeof(float));
+      gw[9] = bb[0];
+      gw[10] = pa[0];
+    }
+    h->gate = pk.add(gw);
+  }
+  if (hipMalloc(&h->dparams, pk.blob.size() * sizeof(float)) != hipSuccess ||
+      hipMemcpy(h->dparams, pk.blob.data(), pk.blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    g_err = "device allocation/upload of the packed weights failed";
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N) {
+  if (!h || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_reserve: bad arguments");
+  DeviceGuard dg(h->device);
+  return ws_reserve(h, B, N);
+}
+
+int32_t sepvad_set_timing(sepvad_handle h, int32_t on) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  h->timing = on != 0;
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, double* total_ms) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  if (gemm_ms) { gemm_ms[0] = h->gemm_ms; gemm_ms[1] = h->g2_ms; }
+  if (gemm_launches) { gemm_launches[0] = h->gemm_launches; gemm_launches[1] = h->g2_launches; }
+  if (total_ms) *total_ms = h->total_ms;
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, const SepVadOutputs* out,
+                       const SepVadInferKw* kw, void* stream) {
+  if (!h || !x || !out || !out->sep) return fail(SEPVAD_E_ARG, "sepvad_forward: null argument");
+  if (B < 1) return fail(SEPVAD_E_SHAPE, "sepvad_forward: B must be >= 1");
+  if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
+  const int T = 1 + N / HOP;
+  const int Tp = round_up(T, TILE);
+  if (Tp > 1024) return fail(SEPVAD_E_SHAPE, "sepvad_forward: at most 1023 STFT frames (N < 261888) per call; "
+                                             "use the streaming wrapper for longer inputs");
+  DeviceGuard dg(h->device);
+  int rc = ws_reserve(h, B, N);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const SepVadConfig& c = h->cfg;
+  Workspace& w = h->ws;
+  const int ntu = Tp / TILE;
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  h->ev.clear();
+  std::vector<int> gemm_ev, g2_ev;
+  if (ev_record(h, s)) return SEPVAD_E_HIP;
+
+  // 1. STFT (spec_input for the spectrum, spec_output for est; identical windows -> one pass)
+  {
+    StftArgs sa{};
+    sa.B = B; sa.N = N; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
+    sa.window = h->P(h->win_out);
+    sa.X = w.X;
+    sa.specdb = h->same_stft_window ? w.specdb : nullptr;
+    HIPCHK(launch_stft(sa, s));
+    if (!h->same_stft_window) {
+      sa.window = h->P(h->win_in);
+      sa.X = nullptr;
+      sa.specdb = w.specdb;
+      HIPCHK(launch_stft(sa, s));
+    }
+  }
+  // 2. activity gate + TCN.LN statistics
+  {
+    GateArgs ga{};
+    ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
+    ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = w.S0; ga.spec_side = out->spectrum;
+    ga.out_slots = w.sl_gate;
+    HIPCHK(launch_gate(ga, s));
+  }
+  // 3. TCN blocks
+  int cur = 0;  // w.O[cur] holds the current block input o after G1 materializes it
+  for (int i = 0; i < h->nblk; ++i) {
+    const BlockOff& bo = h->blk[i];
+    const int nxt = (i == 0) ? 0 : (cur ^ 1);
+    GemmArgs g{};
+    g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH;
+    g.WT = h->P(bo.w1t); g.bias = h->P(bo.b1); g.prelu = bo.a1;
+    if (i == 0) {
+      g.ld.mode = LD_GN; g.ld.X = w.S0;
+      g.ld.g1 = h->P(h->ln_g); g.ld.be1 = h->P(h->ln_b); g.ld.eps1 = 1e-8f;
+      g.ld.slots = w.sl_gate; g.ld.nslots = gate_tiles();
+    } else {
+      g.ld = residual_spec(h, i - 1, w.O[cur], w.U);
+    }
+    g.Xmat = w.O[nxt];
+    g.Y = w.A; g.out_slots = w.sl_g1;
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    gemm_ev.push_back((int)h->ev.size() - 2);
+    cur = nxt;
+
+    DwArgs d{};
+    d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
+    d.slots = w.sl_g1; d.nslots = (CH / TILE) * ntu;
+    d.g1 = h->P(bo.g1); d.be1 = h->P(bo.be1); d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
+    d.D = w.D; d.out_slots = w.sl_dw;
+    HIPCHK(launch_dw(d, s));
+
+    GemmArgs g2{};
+    g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID;
+    g2.WT = h->P(bo.w2t); g2.bias = h->P(bo.b2);
+    g2.ld.mode = LD_GN; g2.ld.X = w.D; g2.ld.g1 = h->P(bo.g2); g2.ld.be1 = h->P(bo.be2); g2.ld.eps1 = 1e-8f;
+    g2.ld.slots = w.sl_dw; g2.ld.nslots = CH / 16;
+    g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    gemm_ev.push_back((int)h->ev.size() - 2);
+    g2_ev.push_back((int)h->ev.size() - 2);
+
+    AttArgs at{};
+    at.B = B; at.T = T; at.Tp = Tp; at.mtiles = CH / TILE; at.ntiles = ntu; at.tf_att = c.tf_attention;
+    at.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
+    at.R = w.R; at.O = w.O[cur]; at.colsum = w.colsum; at.rowsum = w.rowsum; at.attp = h->P(bo.attp);
+    at.U = w.U; at.moments = w.moments; at.out_slots = w.sl_att;
+    HIPCHK(launch_att(at, s));
+  }
+  // 4. output head: PReLU -> GN(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
+  {
+    HeadPrepArgs hp{};
+    hp.B = B; hp.T = T; hp.Tp = Tp;
+    hp.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.U);
+    hp.alpha = h->out_a; hp.P = w.P; hp.out_slots = w.sl_hp;
+    HIPCHK(launch_head_prep(hp, s));
+    GemmArgs g{};
+    g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = 2 * NBIN; g.K = CH;
+    g.WT = h->P(h->wot); g.bias = h->P(h->bo);
+    g.ld.mode = LD_GN; g.ld.X = w.P; g.ld.g1 = h->P(h->out_g); g.ld.be1 = h->P(h->out_b); g.ld.eps1 = 1e-5f;
+    g.ld.slots = w.sl_hp; g.ld.nslots = CH / 16;
+    g.Y = w.masks; g.Yside = out->masks_b;
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    gemm_ev.push_back((int)h->ev.size() - 2);
+  }
+  // 5. VAD head + inference-only smoothing (model/model.py:424-427,434-436,444-457)
+  const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
+  const bool kw_on = kw && kw->enabled && c.final_vad;
+  if (has_vad) {
+    VadArgs v{};
+    v.B = B; v.T = T; v.Tp = Tp; v.masked_speakers = c.final_vad_masked_speakers; v.noisy_phase = c.noisy_phase;
+    v.masks = w.masks; v.X = w.X;
+    v.w1 = h->P(h->v_w1); v.b1 = h->P(h->v_b1); v.alpha = h->v_a; v.g = h->P(h->v_g); v.be = h->P(h->v_b);
+    v.w2 = h->P(h->v_w2); v.b2 = h->v_b2;
+    v.kw_enabled = kw_on;
+    v.filt = kw_on && (kw->filter_signals_by_smo_vad || kw->filter_signals_by_unsmo_vad);
+    v.ret_smooth = kw_on && kw->return_smoothed_vad;
+    v.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
+    v.vad_out = out->vad ? out->vad : w.vad;
+    v.gain = w.gain;
+    HIPCHK(launch_vad(v, s));
+  }
+  // 6. est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-439,452-455,460)
+  {
+    IstftArgs is{};
+    is.BS = B * 2; is.S = 2; is.N = N; is.T = T; is.Tp = Tp; is.noisy_phase = c.noisy_phase; is.est_mode = 1;
+    is.X = w.X; is.masks = w.masks; is.gain = (has_vad && kw_on) ? w.gain : nullptr;
+    is.window = h->P(h->win_inv); is.tw = (const float2*)h->P(h->tw);
+    is.est_out = (float2*)out->est; is.mask_out = out->mask; is.y = out->sep;
+    HIPCHK(launch_istft(is, s));
+  }
+  if (ev_record(h, s)) return SEPVAD_E_HIP;
+  if (h->timing) {
+    HIPCHK(hipEventSynchronize(h->ev.back()));
+    h->gemm_ms = h->g2_ms = 0.0;
+    for (int k : gemm_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->gemm_ms += ms; }
+    for (int k : g2_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->g2_ms += ms; }
+    float tot; HIPCHK(hipEventElapsedTime(&tot, h->ev.front(), h->ev.back()));
+    h->total_ms = tot;
+    h->gemm_launches = (int)gemm_ev.size();
+    h->g2_launches = (int)g2_ev.size();
+  }
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {
+  if (!h || !x || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_stft: bad arguments");
+  DeviceGuard dg(h->device);
+  const int T = 1 + N / HOP;
+  StftArgs sa{};
+  sa.B = B; sa.N = N; sa.T = T; sa.Tp = round_up(T, TILE); sa.x = x;
+  sa.window = h->P(h->win_out); sa.tw = (const float2*)h->P(h->tw);
+  sa.Xout = (float2*)X; sa.spec_out = h->same_stft_window ? spec : nullptr;
+  HIPCHK(launch_stft(sa, (hipStream_t)stream));
+  if (!h->same_stft_window && spec) {
+    sa.window = h->P(h->win_in); sa.Xout = nullptr; sa.spec_out = spec;
+    HIPCHK(launch_stft(sa, (hipStream_t)stream));
+  }
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_istft(sepvad_handle h, const void* est, int32_t BS, int32_t N, float* y, void* stream) {
+  if (!h || !est || !y || BS < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_istft: bad arguments");
+  DeviceGuard dg(h->device);
+  const int T = 1 + N / HOP;
+  IstftArgs is{};
+  is.BS = BS; is.S = 1; is.N = N; is.T = T; is.Tp = round_up(T, TILE); is.est_mode = 0;
+  is.est_in = (const float2*)est; is.window = h->P(h->win_inv); is.tw = (const float2*)h->P(h->tw); is.y = y;
+  HIPCHK(launch_istft(is, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+void sepvad_destroy(sepvad_handle h) {
+  if (!h) return;
+  DeviceGuard dg(h->device);
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  if (h->ws.base) (void)hipFree(h->ws.base);
+  if (h->dparams) (void)hipFree(h->dparams);
+  delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+"""Drop-in ``SeparationModel`` (reference ``model/model.py:360-461``) backed by MI355X HIP kernels.
+
+The module tree registers exactly the reference's parameters and buffers (state_dict keys of
+``config.param_spec``), so ``load_state_dict(checkpoint['state_dict'], strict=True)`` works with a
+reference checkpoint. ``forward`` keeps the reference contract:
+
+* ``assert x.ndim == 2`` (model/model.py:406) — the only validation the reference does;
+* returns ``(sep [B,num_spk,N] f32, vad, est [B,num_spk,257,T] complex64)`` where ``vad`` is
+  ``[B,num_spk,T]`` probabilities, ``[B,num_spk,1,T]`` {0,1} when
+  ``inference_kw['return_smoothed_vad']``, or the int 0 when ``final_vad`` is False
+  (model/model.py:424-427,456-457,461);
+* sets ``self.spectrum``, ``self.masks_b``, ``self.mask_per_speaker`` (post-sigmoid) and
+  ``self.estimated_stfts`` (model/model.py:412,421,429,437-439).
+
+All arithmetic runs in ``libsepvad.so`` through the C ABI of ``include/sepvad.h``; there is no
+CPU fallback — a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import config as _config
+from . import native as _native
+
+
+class _WNConv(nn.Module):
+    """Parameter holder of a weight-normed conv: bias, weight_g, weight_v (torch weight_norm)."""
+
+    def __init__(self, cout, cin_per_group, k):
+        super().__init__()
+        self.bias = nn.Parameter(torch.zeros(cout))
+        self.weight_g = nn.Parameter(torch.ones(cout, 1, 1))
+        self.weight_v = nn.Parameter(torch.ones(cout, cin_per_group, k))
+
+
+class _Conv(nn.Module):
+    def __init__(self, wshape):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(*wshape))
+        self.bias = nn.Parameter(torch.zeros(wshape[0]))
+
+
+class _GN(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+
+
+class _PReLU(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.weight = nn.Parameter(torch.full((1,), 0.25))
+
+
+class _Window(nn.Module):
+    def __init__(self, n):
+        super().__init__()
+        self.register_buffer("window", torch.hann_window(n))
+
+
+class _InputSpec(nn.Module):
+    def __init__(self, n):
+        super().__init__()
+        self.spec = _Window(n)
+
+
+class _DepthConv1d(nn.Module):
+    """Parameters of DepthConv1d, weight-normed branch (model/model.py:103-127)."""
+
+    def __init__(self, C, H):
+        super().__init__()
+        self.conv1d = _WNConv(C, C, 1)
+        self.dconv1d = _WNConv(H, 1, 3)
+        self.res_out = _WNConv(C, H, 1)
+        self.nonlinearity1 = _PReLU()
+        self.nonlinearity2 = _PReLU()
+        self.reg1 = _GN(C)
+        self.reg2 = _GN(H)
+
+
+class _TFAttention(nn.Module):
+    """Parameters of TF_Attention (model/model.py:182-195)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1d_t_1 = _Conv((1, 1, 3))
+        self.conv1d_t_2 = _Conv((1, 1, 3))
+        self.prelu_t = _PReLU()
+        self.conv1d_f_1 = _Conv((1, 1, 3))
+        self.conv1d_f_2 = _Conv((1, 1, 3))
+        self.prelu_f = _PReLU()
+
+
+class _TCN(nn.Module):
+    """Parameters of TCN, weight-normed branch (model/model.py:271-325)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        C, H = cfg["BN_dim"], cfg["H_dim"]
+        nblk = cfg["layer"] * cfg["stack"]
+        F = cfg["n_fftBins"] // 2 + 1
+        self.LN = _GN(C)
+        self.TCN = nn.ModuleList([_DepthConv1d(C, H) for _ in range(nblk)])
+        if cfg["tf_attention"]:
+            self.time_freq_attnetion = nn.ModuleList([_TFAttention() for _ in range(nblk)])
+        if cfg["apply_recursive_ln"]:
+            self.ln_first_modules = nn.ModuleList([_GN(C) for _ in range(nblk)])
+            self.ln_second_modules = nn.ModuleList([_GN(C) for _ in range(nblk)])
+        if cfg["apply_residual_ln"]:
+            self.ln_modules = nn.ModuleList([_GN(C) for _ in range(nblk)])
+        self.output = nn.Sequential(_PReLU(), _GN(C), _WNConv(F * cfg["num_spk"], C, 1))
+
+
+class _VAD(nn.Module):
+    """Parameters of VAD (model/model.py:153-171)."""
+
+    def __init__(self, F):
+        super().__init__()
+        self.common = nn.Sequential()
+        self.common.add_module("conv1_1", _WNConv(4, F, 5))
+        self.common.add_module("relu_1", _PReLU())
+        self.common.add_module("BN_1", _GN(4))
+        self.output_layer_vad = _WNConv(1, 4, 3)
+
+
+class SeparationModel(nn.Module):
+    """Sep-TFAnet^VAD separator; same kwargs as the reference (model/model.py:361-366)."""
+
+    def __init__(self, **config):
+        super().__init__()
+        cfg = _config.merge_config(config)
+        print(cfg)  # the reference prints the merged defaults (model/model.py:371)
+        for key, value in cfg.items():
+            setattr(self, key, value)
+        self._cfg = cfg
+        why = _config.native_support_error(cfg)
+        if why is not None:
+            raise NotImplementedError(f"SeparationModel: {why}")
+        n = cfg["n_fftBins"]
+        self.n_fftBins_h = n // 2 + 1
+        self.spec_input = _InputSpec(n)
+        self.spec_output = _Window(n)
+        self.inv_spec = _Window(n)
+        self.TCN = _TCN(cfg)
+        if cfg["final_vad"]:
+            self.vad = _VAD(self.n_fftBins_h)
+        if cfg["activity_input_bool"]:
+            self.activity_input = _Conv((1, 1, 3, 3))
+            self.prelu = _PReLU()
+        self._handles = {}
+        self.register_load_state_dict_post_hook(lambda module, keys: module._invalidate_native())
+
+    # -- native handle -------------------------------------------------------------------------
+    # The handle (folded, packed device weights) is rebuilt lazily after load_state_dict(),
+    # .to()/.cuda()/.float() (both invalidate it), or an explicit refresh_native() — call that
+    # after editing parameters in place.
+    def _invalidate_native(self, *args, **kwargs):
+        self._handles = {}
+
+    def refresh_native(self):
+        self._invalidate_native()
+
+    def _apply(self, fn, *args, **kwargs):
+        self._invalidate_native()
+        return super()._apply(fn, *args, **kwargs)
+
+    def native_handle(self, device=None):
+        """The C-ABI handle for ``device`` (built from the current weights on first use)."""
+        device = torch.device(device) if device is not None else next(self.parameters()).device
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        h = self._handles.get(device)
+        if h is None:
+            sd = {k: v.detach() for k, v in self.state_dict().items()}
+            h = _native.Handle(self._cfg, sd, device)
+            self._handles[device] = h
+        return h
+
+    # -- forward (model/model.py:402-461) --------------------------------------------------------
+    def forward(self, x: torch.Tensor, inference_kw: dict = {}):  # noqa: B006  (reference signature)
+        assert x.ndim == 2, "input tensor must be 2 dimensions (B, T), but got dimensions of {}".format(x.ndim)
+        if x.device.type != "cuda":
+            raise RuntimeError("SeparationModel (MI355X build) runs on a ROCm device only: "
+                               "move the model and the input to 'cuda' (there is no CPU path)")
+        h = self.native_handle(x.device)
+        out = h.forward(x, inference_kw if inference_kw else None, return_aux=True)
+        self.spectrum = out["spectrum"]
+        self.masks_b = out["masks_b"]
+        self.mask_per_speaker = out["mask_per_speaker"]
+        self.estimated_stfts = out["est"]
+        return out["sep"], out["vad"], out["est"]

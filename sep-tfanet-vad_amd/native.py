@@ -1,0 +1,226 @@
+"""ctypes binding of ``libsepvad.so`` (C ABI declared in ``include/sepvad.h``).
+
+This is the reference-side binding a Python caller of the boundary needs; ``model.py`` uses it to
+keep the reference's ``SeparationModel`` surface. The library is built in-tree by
+``__graft_entry__.build()`` (``make -C sep-tfanet-vad_amd/csrc``). There is no fallback: a missing
+library, a CPU tensor or a non-zero status raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsepvad.so")
+
+SEPVAD_LN_PLAIN, SEPVAD_LN_RECURSIVE, SEPVAD_LN_RESIDUAL = 0, 1, 2
+SEPVAD_PREC_FP32 = 0
+
+EXPORTED_SYMBOLS = (
+    "sepvad_create", "sepvad_reserve", "sepvad_forward", "sepvad_stft", "sepvad_istft",
+    "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
+)
+
+
+class SepVadConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_fft", "bn_dim", "h_dim", "layer", "stack", "num_spk", "tf_attention", "ln_mode",
+        "final_vad", "final_vad_masked_speakers", "noisy_phase", "activity_input", "precision")]
+
+
+class SepVadInferKw(ctypes.Structure):
+    _fields_ = [("enabled", ctypes.c_int32), ("filter_signals_by_smo_vad", ctypes.c_int32),
+                ("filter_signals_by_unsmo_vad", ctypes.c_int32), ("length_smoothing_filter", ctypes.c_int32),
+                ("threshold_activated_vad", ctypes.c_float), ("return_smoothed_vad", ctypes.c_int32)]
+
+
+class SepVadOutputs(ctypes.Structure):
+    _fields_ = [("sep", ctypes.c_void_p), ("vad", ctypes.c_void_p), ("est", ctypes.c_void_p),
+                ("spectrum", ctypes.c_void_p), ("masks_b", ctypes.c_void_p), ("mask", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libsepvad.so (after torch, so it binds to torch's HIP runtime) and declare signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libsepvad.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` or `make -C sep-tfanet-vad_amd/csrc`")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    i32 = ctypes.c_int32
+    lib.sepvad_create.restype = P
+    lib.sepvad_create.argtypes = [ctypes.POINTER(SepVadConfig), ctypes.POINTER(P), ctypes.POINTER(ctypes.c_char_p),
+                                  ctypes.POINTER(ctypes.c_int64), i32, i32]
+    lib.sepvad_reserve.restype = i32
+    lib.sepvad_reserve.argtypes = [P, i32, i32]
+    lib.sepvad_forward.restype = i32
+    lib.sepvad_forward.argtypes = [P, P, i32, i32, ctypes.POINTER(SepVadOutputs), ctypes.POINTER(SepVadInferKw), P]
+    lib.sepvad_stft.restype = i32
+    lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
+    lib.sepvad_istft.restype = i32
+    lib.sepvad_istft.argtypes = [P, P, i32, i32, P, P]
+    lib.sepvad_set_timing.restype = i32
+    lib.sepvad_set_timing.argtypes = [P, i32]
+    lib.sepvad_timing.restype = i32
+    lib.sepvad_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double)]
+    lib.sepvad_destroy.restype = None
+    lib.sepvad_destroy.argtypes = [P]
+    lib.sepvad_last_error.restype = ctypes.c_char_p
+    lib.sepvad_last_error.argtypes = []
+    lib.sepvad_abi_version.restype = i32
+    lib.sepvad_abi_version.argtypes = []
+    _lib = lib
+    return lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = _lib.sepvad_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def make_config(cfg: dict) -> SepVadConfig:
+    c = SepVadConfig()
+    c.n_fft, c.bn_dim, c.h_dim = cfg["n_fftBins"], cfg["BN_dim"], cfg["H_dim"]
+    c.layer, c.stack, c.num_spk = cfg["layer"], cfg["stack"], cfg["num_spk"]
+    c.tf_attention = int(bool(cfg["tf_attention"]))
+    c.ln_mode = (SEPVAD_LN_RECURSIVE if cfg["apply_recursive_ln"] else
+                 SEPVAD_LN_RESIDUAL if cfg["apply_residual_ln"] else SEPVAD_LN_PLAIN)
+    c.final_vad = int(bool(cfg["final_vad"]))
+    c.final_vad_masked_speakers = int(bool(cfg["final_vad_masked_speakers"]))
+    c.noisy_phase = int(bool(cfg["noisy_phase"]))
+    c.activity_input = int(bool(cfg["activity_input_bool"]))
+    c.precision = SEPVAD_PREC_FP32
+    return c
+
+
+def make_kw(inference_kw) -> SepVadInferKw | None:
+    """inference_kw dict -> struct (None or {} == the reference's skipped branch, model/model.py:444)."""
+    if not inference_kw:
+        return None
+    k = SepVadInferKw()
+    k.enabled = 1
+    # the reference indexes these keys directly (KeyError if absent) — keep that behaviour
+    k.filter_signals_by_smo_vad = int(bool(inference_kw["filter_signals_by_smo_vad"]))
+    k.filter_signals_by_unsmo_vad = int(bool(inference_kw["filter_signals_by_unsmo_vad"]))
+    k.length_smoothing_filter = int(inference_kw["length_smoothing_filter"])
+    k.threshold_activated_vad = float(inference_kw["threshold_activated_vad"])
+    k.return_smoothed_vad = int(bool(inference_kw["return_smoothed_vad"]))
+    return k
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class Handle:
+    """Owns one ``sepvad_handle`` (device weights + workspace) for one device."""
+
+    def __init__(self, cfg: dict, state_dict: dict, device):
+        lib = load_library()
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("libsepvad needs a ROCm device")
+        self.device = device
+        self.index = device.index if device.index is not None else torch.cuda.current_device()
+        self.cfg = dict(cfg)
+        host = [(k, v.detach().to("cpu", torch.float32).contiguous()) for k, v in state_dict.items()
+                if torch.is_floating_point(v)]
+        n = len(host)
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, t in host])
+        names = (ctypes.c_char_p * n)(*[k.encode() for k, _ in host])
+        numels = (ctypes.c_int64 * n)(*[t.numel() for _, t in host])
+        self._c = make_config(cfg)
+        h = lib.sepvad_create(ctypes.byref(self._c), ptrs, names, numels, n, self.index)
+        if not h:
+            raise RuntimeError("sepvad_create failed: " + lib.sepvad_last_error().decode(errors="replace"))
+        self._h = ctypes.c_void_p(h)
+        self._lib = lib
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.sepvad_destroy(h)
+            self._h = None
+
+    @property
+    def raw(self):
+        return self._h
+
+    def reserve(self, B: int, N: int):
+        _check(self._lib.sepvad_reserve(self._h, B, N), "sepvad_reserve")
+
+    def set_timing(self, on: bool):
+        _check(self._lib.sepvad_set_timing(self._h, int(on)), "sepvad_set_timing")
+
+    def timing(self):
+        ms = (ctypes.c_double * 2)()
+        cnt = (ctypes.c_int32 * 2)()
+        tot = ctypes.c_double()
+        _check(self._lib.sepvad_timing(self._h, ms, cnt, ctypes.byref(tot)), "sepvad_timing")
+        return dict(gemm_ms=ms[0], res_out_ms=ms[1], gemm_launches=cnt[0], res_out_launches=cnt[1], total_ms=tot.value)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def forward(self, x: torch.Tensor, inference_kw=None, return_aux: bool = False, outputs: dict | None = None):
+        """One forward. Returns dict(sep, vad, est[, spectrum, masks_b, mask_per_speaker])."""
+        if x.device.type != "cuda":
+            raise RuntimeError("sepvad forward: input must be a ROCm device tensor")
+        x = x.to(self.device, torch.float32).contiguous()
+        B, N = x.shape
+        T = 1 + N // (self.cfg["n_fftBins"] // 2)
+        F = self.cfg["n_fftBins"] // 2 + 1
+        S = self.cfg["num_spk"]
+        dev = self.device
+        o = outputs or {}
+        sep = o.get("sep") if o.get("sep") is not None else torch.empty(B, S, N, device=dev, dtype=torch.float32)
+        has_vad = bool(self.cfg["final_vad"]) and (not self.cfg["final_vad_masked_speakers"] or self.cfg["noisy_phase"])
+        vad = (o.get("vad") if o.get("vad") is not None else torch.empty(B, S, T, device=dev, dtype=torch.float32)) \
+            if has_vad else None
+        est = o.get("est") if o.get("est") is not None else torch.empty(B, S, F, T, device=dev, dtype=torch.complex64)
+        spectrum = masks_b = mask = None
+        if return_aux:
+            spectrum = torch.empty(B, F, T, device=dev, dtype=torch.float32)
+            masks_b = torch.empty(B, S * F, T, device=dev, dtype=torch.float32)
+            mask = torch.empty(B, S, F, T, device=dev, dtype=torch.float32)
+        outs = SepVadOutputs(_ptr(sep).value, _ptr(vad).value, _ptr(est).value, _ptr(spectrum).value,
+                             _ptr(masks_b).value, _ptr(mask).value)
+        kw = make_kw(inference_kw)
+        rc = self._lib.sepvad_forward(self._h, _ptr(x), B, N, ctypes.byref(outs),
+                                      ctypes.byref(kw) if kw is not None else None, self._stream())
+        _check(rc, "sepvad_forward")
+        if vad is None:
+            vad_ret = 0  # model/model.py:427
+        elif kw is not None and kw.return_smoothed_vad:
+            vad_ret = vad.view(B, S, 1, T)  # model/model.py:456-457
+        else:
+            vad_ret = vad
+        res = dict(sep=sep, vad=vad_ret, est=est)
+        if return_aux:
+            res.update(spectrum=spectrum, masks_b=masks_b, mask_per_speaker=mask)
+        return res
+
+    def stft(self, x: torch.Tensor):
+        """STFT with DC zeroed and its dB spectrum (kernel-level test entry)."""
+        x = x.to(self.device, torch.float32).contiguous()
+        B, N = x.shape
+        T = 1 + N // 256
+        X = torch.empty(B, 257, T, device=self.device, dtype=torch.complex64)
+        spec = torch.empty(B, 257, T, device=self.device, dtype=torch.float32)
+        _check(self._lib.sepvad_stft(self._h, _ptr(x), B, N, _ptr(X), _ptr(spec), self._stream()), "sepvad_stft")
+        return X, spec
+
+    def istft(self, est: torch.Tensor, N: int):
+        """torch.istft(center=True, length=N) of est [BS, 257, T] complex64 (kernel-level test entry)."""
+        est = est.to(self.device, torch.complex64).contiguous()
+        BS = est.shape[0]
+        y = torch.empty(BS, N, device=self.device, dtype=torch.float32)
+        _check(self._lib.sepvad_istft(self._h, _ptr(est), BS, N, _ptr(y), self._stream()), "sepvad_istft")
+        return y

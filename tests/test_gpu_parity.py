@@ -1,0 +1,171 @@
+"""Parity of the HIP path (through the C ABI) with the reference's golden outputs and the oracle.
+
+Gates: separated waveforms max-abs <= 1e-4 (fp32 path); thresholded VAD labels
+bit-exact; SI-SDR within 0.01 dB. Kernel-level checks compare against plain PyTorch fp32 ops.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import CASES, CONFIGS, config_of, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SEP_TOL = 1e-4   # north_star: waveform max-abs
+DEV = "cuda"
+
+
+def _model(cname, state_dicts):
+    import sep_tfanet_vad_amd as pkg
+    net = pkg.SeparationModel(**config_of(cname))
+    net.load_state_dict(state_dicts[cname], strict=True)
+    return net.eval().to(DEV)
+
+
+@pytest.fixture(scope="module")
+def models(state_dicts):
+    return {c: _model(c, state_dicts) for c in CONFIGS}
+
+
+def test_native_library_is_loaded():
+    from sep_tfanet_vad_amd import native
+    lib = native.load_library()
+    assert lib.sepvad_abi_version() == 1
+    assert torch.cuda.is_available()
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+@pytest.mark.parametrize("case", CASES)
+def test_forward_matches_reference(cname, case, models):
+    g = load_golden(cname, case)
+    net = models[cname]
+    x = torch.from_numpy(g["x"]).to(DEV)
+    with torch.no_grad():
+        sep, vad, est = net(x)
+    torch.cuda.synchronize()
+    sep, vad = sep.cpu().numpy(), vad.cpu().numpy()
+    err = np.abs(sep - g["sep"]).max()
+    assert err <= SEP_TOL, f"sep max-abs {err}"
+    assert vad.shape == g["vad"].shape
+    assert np.array_equal(vad >= 0.5, g["vad"] >= 0.5), "VAD labels differ"
+    assert np.abs(vad - g["vad"]).max() <= 1e-4
+    assert np.abs(net.masks_b.cpu().numpy() - g["masks_b"]).max() <= 2e-3
+    assert np.abs(net.spectrum.cpu().numpy() - g["spectrum"]).max() <= 0.2
+    mps = torch.sigmoid(torch.from_numpy(g["masks_b"])).reshape(net.mask_per_speaker.shape).numpy()
+    assert np.abs(net.mask_per_speaker.cpu().numpy() - mps).max() <= 1e-3
+    if "est_re" in g:
+        e = est.cpu()
+        assert e.dtype == torch.complex64 and tuple(e.shape) == g["est_re"].shape
+        assert np.abs(e.real.numpy() - g["est_re"]).max() <= 1e-3
+        assert np.abs(e.imag.numpy() - g["est_im"]).max() <= 1e-3
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_inference_kw_smoothed_vad(cname, models):
+    g = load_golden(cname, "small")
+    ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+               threshold_activated_vad=0.5, return_smoothed_vad=True)
+    with torch.no_grad():
+        sep, vad, _ = models[cname](torch.from_numpy(g["x"]).to(DEV), ikw)
+    assert tuple(vad.shape) == g["ikw_vad"].shape  # [B, 2, 1, T]
+    assert np.array_equal(vad.cpu().numpy(), g["ikw_vad"])
+    assert np.abs(sep.cpu().numpy() - g["ikw_sep"]).max() <= SEP_TOL
+
+
+def test_inference_kw_variants_vs_oracle(models, state_dicts):
+    """unsmoothed-filter flag, threshold, length_smoothing_filter=5 (no effect) vs the oracle."""
+    from oracle.torch_ref import OracleModel
+    g = load_golden("with_vad", "small")
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"])
+    x = torch.from_numpy(g["x"])
+    for ikw in (dict(filter_signals_by_smo_vad=False, filter_signals_by_unsmo_vad=True, length_smoothing_filter=5,
+                     threshold_activated_vad=0.4, return_smoothed_vad=False),
+                dict(filter_signals_by_smo_vad=False, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+                     threshold_activated_vad=0.6, return_smoothed_vad=True)):
+        s_ref, v_ref, _ = om(x, ikw)
+        with torch.no_grad():
+            s, v, _ = models["with_vad"](x.to(DEV), ikw)
+        assert tuple(v.shape) == tuple(v_ref.shape)
+        assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+        if ikw["return_smoothed_vad"]:
+            assert np.array_equal(v.cpu().numpy(), v_ref.numpy())
+
+
+def test_stft_kernel_vs_torch(models):
+    """STFT kernel vs torch.stft (fp32, on the GPU) — the op torchaudio.Spectrogram runs."""
+    h = models["with_vad"].native_handle(DEV)
+    for N in (8000, 12345, 32000, 257):
+        x = torch.rand(3, N, device=DEV) * 1.8 - 0.9
+        X, spec = h.stft(x)
+        win = torch.hann_window(512, device=DEV)
+        Xr = torch.stft(x, 512, 256, 512, win, center=True, pad_mode="reflect", normalized=False, onesided=True,
+                        return_complex=True)
+        Xr[:, 0, :] = 0
+        assert X.shape == Xr.shape
+        assert (X - Xr).abs().max().item() <= 2e-5 * Xr.abs().max().item() + 1e-5
+        sr = 10 * torch.log10(torch.clamp(Xr.abs() ** 2, min=1e-10))
+        ok = Xr.abs() > 1e-3
+        assert (spec - sr)[ok].abs().max().item() <= 1e-3
+
+
+def test_istft_kernel_vs_torch(models):
+    h = models["with_vad"].native_handle(DEV)
+    for N in (8000, 12345, 32000):
+        T = 1 + N // 256
+        est = torch.randn(4, 257, T, device=DEV, dtype=torch.complex64)
+        y = h.istft(est, N)
+        win = torch.hann_window(512, device=DEV)
+        yr = torch.istft(est, 512, 256, 512, win, center=True, normalized=False, onesided=True, length=N)
+        assert (y - yr).abs().max().item() <= 1e-5 * max(1.0, yr.abs().max().item())
+
+
+def test_stft_istft_round_trip(models):
+    h = models["with_vad"].native_handle(DEV)
+    x = torch.rand(2, 32000, device=DEV) * 1.8 - 0.9
+    X, _ = h.stft(x)
+    # DC was removed: the round trip reproduces x minus its per-frame DC contribution; compare with torch
+    win = torch.hann_window(512, device=DEV)
+    yr = torch.istft(X, 512, 256, 512, win, center=True, length=32000)
+    y = h.istft(X, 32000)
+    assert (y - yr).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_full_batch_properties(cname, models, state_dicts):
+    """BASELINE cfg shape B=64, N=32000: a sample of utterances vs the oracle, batch invariance
+    (bitwise), determinism, and SI-SDR within 0.01 dB of the oracle against the clean sources."""
+    from oracle.torch_ref import OracleModel, si_sdr
+    from sep_tfanet_vad_amd import synth
+    B, N = 64, 32000
+    x, srcs = synth.make_batch(B, N, 5000)
+    xd = torch.from_numpy(x).to(DEV)
+    net = models[cname]
+    with torch.no_grad():
+        sep, vad, est = net(xd)
+        sep2, vad2, _ = net(xd)
+        sub = [0, 17, 63]
+        sep_sub, vad_sub, _ = net(xd[sub])
+    torch.cuda.synchronize()
+    assert torch.equal(sep, sep2) and torch.equal(vad, vad2)           # deterministic
+    assert torch.equal(sep[sub], sep_sub) and torch.equal(vad[sub], vad_sub)  # batch invariant
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    s_ref, v_ref, _ = om(torch.from_numpy(x[sub]))
+    assert np.abs(sep_sub.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((vad_sub.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    # SI-SDR (reference model/combined_loss.py:16-56) of each output vs the matching source
+    tgt = torch.from_numpy(srcs[sub])
+    d = (si_sdr(sep_sub.cpu(), tgt) - si_sdr(s_ref, tgt)).abs().max().item()
+    assert d <= 0.01, f"SI-SDR differs by {d} dB"
+
+
+def test_streams_and_devices_do_not_leak_state(models):
+    """Two handles / back-to-back shapes: results depend only on the inputs."""
+    g = load_golden("with_vad", "ragged")
+    net = models["with_vad"]
+    with torch.no_grad():
+        a, _, _ = net(torch.from_numpy(g["x"]).to(DEV))
+        net(torch.rand(5, 48000, device=DEV))  # grow the workspace
+        b, _, _ = net(torch.from_numpy(g["x"]).to(DEV))
+    assert torch.equal(a, b)

@@ -1,0 +1,96 @@
+"""The oracle (CPU restatement, oracle/torch_ref.py) pinned against the reference's own outputs.
+
+Golden vectors were produced by running the reference forward (tests/golden/make_golden.py).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CASES, CONFIGS, config_of, load_golden
+from oracle.torch_ref import OracleModel, si_sdr
+
+
+def _sha(sd):
+    h = hashlib.sha256()
+    for k, v in sd.items():
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v.numpy(), dtype=np.float32).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_recipe_weights_match_fixture(cname, state_dicts):
+    g = load_golden(cname, "small")
+    assert str(g["weights_sha256"]) == _sha(state_dicts[cname])
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_fp32_matches_reference(cname, case, state_dicts):
+    g = load_golden(cname, case)
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    sep, vad, est = om(torch.from_numpy(g["x"]))
+    assert np.abs(sep.numpy() - g["sep"]).max() <= 2e-6
+    assert np.abs(vad.numpy() - g["vad"]).max() <= 2e-5
+    assert np.abs(om.masks_b.numpy() - g["masks_b"]).max() <= 5e-5
+    assert np.abs(om.spectrum.numpy() - g["spectrum"]).max() <= 1e-3
+    assert np.array_equal(vad.numpy() >= 0.5, g["vad"] >= 0.5)
+    if "est_re" in g:
+        assert np.abs(est.real.numpy() - g["est_re"]).max() <= 1e-4
+        assert np.abs(est.imag.numpy() - g["est_im"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_oracle_intermediates(cname, state_dicts):
+    g = load_golden(cname, "small")
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    o0 = om.block_io(torch.from_numpy(g["x"]), 0)
+    assert np.abs(o0.numpy() - g["tcn_in"]).max() <= 1e-5
+    r0 = om.depthconv(om.blocks[0], o0, om.dil[0])
+    assert np.abs(r0.numpy() - g["blk0_res"]).max() <= 1e-4
+    a0 = om.tf_attention(0, r0)
+    assert np.abs(a0.numpy() - g["blk0_att"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_oracle_inference_kw_branch(cname, state_dicts):
+    g = load_golden(cname, "small")
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+               threshold_activated_vad=0.5, return_smoothed_vad=True)
+    sep, vad, _ = om(torch.from_numpy(g["x"]), ikw)
+    assert vad.shape == g["ikw_vad"].shape  # [B, 2, 1, T]
+    assert np.array_equal(vad.numpy(), g["ikw_vad"])
+    assert np.abs(sep.numpy() - g["ikw_sep"]).max() <= 2e-6
+
+
+def test_smoothing_known_answer():
+    """model/model.py:444-451: taps [1,0,1], min(.,1), first/last frame copied."""
+    import os
+    from conftest import GOLDEN
+    kat = np.load(os.path.join(GOLDEN, "golden_smoothing_kat.npz"))
+    p = kat["vad"]
+    thr = (p >= 0.5).astype(np.float32)
+    pad = np.concatenate([[0.0], thr, [0.0]])
+    sm = np.minimum(pad[:-2] + pad[2:], 1.0)
+    sm[[0, -1]] = thr[[0, -1]]
+    assert np.array_equal(sm, kat["smoothed"])
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_fp32_reference_noise_floor(cname):
+    """fp32 reference vs its own fp64 run: the budget left under the 1e-4 waveform gate."""
+    g = load_golden(cname, "small")
+    d = np.abs(g["sep"] - g["sep_f64"]).max()
+    assert d < 5e-5
+    # thresholded labels of the fixtures keep a margin above the fp32 noise floor
+    assert np.abs(g["vad"] - 0.5).min() > 1e-4
+
+
+def test_si_sdr_formula():
+    """calc_sisdr known answer, zero_mean=False (reference model/combined_loss.py:29-34 docstring: 18.4030)."""
+    target = torch.tensor([3.0, -0.5, 2.0, 7.0])
+    preds = torch.tensor([2.5, 0.0, 2.0, 8.0])
+    assert abs(float(si_sdr(preds, target, zero_mean=False)) - 18.4030) < 1e-3
