@@ -37,8 +37,11 @@ enum {
 /* TCN residual mode (model/model.py:347-352). */
 enum { SEPVAD_LN_PLAIN = 0, SEPVAD_LN_RECURSIVE = 1, SEPVAD_LN_RESIDUAL = 2 };
 
-/* Arithmetic of the pointwise (1x1) GEMMs. FP32 is the parity path (max-abs <= 1e-4). */
-enum { SEPVAD_PREC_FP32 = 0 };
+/* Arithmetic of the pointwise (1x1) GEMMs. Both meet the fp32 parity gates (max-abs <= 1e-4):
+ *   FP32:  v_mfma_f32_32x32x2_f32 (exact fp32 fma chain);
+ *   F16X3: fp32-equivalent split: x = hi + lo (fp16 each), acc += hi*hi + hi*lo + lo*hi on
+ *          v_mfma_f32_32x32x16_f16 with fp32 accumulation (default; 16x the fp32 MFMA rate per pass). */
+enum { SEPVAD_PREC_FP32 = 0, SEPVAD_PREC_F16X3 = 1 };
 
 /* SeparationModel kwargs that change the computation (model/model.py:362-366). */
 typedef struct SepVadConfig {
@@ -89,6 +92,9 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
 
 /* Pre-size the workspace for up to B utterances of N samples (so forward never allocates). */
 int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N);
+
+/* Switch the GEMM arithmetic of later forwards (SEPVAD_PREC_*); weights for both are resident. */
+int32_t sepvad_set_precision(sepvad_handle h, int32_t precision);
 
 /* Replaces SeparationModel.forward(x, inference_kw) (model/model.py:402-461).
  * x: device [B, N] f32. kw may be NULL (== empty dict). Stream-ordered on `stream`

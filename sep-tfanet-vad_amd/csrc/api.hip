@@ -1,7 +1,15 @@
 // C ABI of libsepvad.so (include/sepvad.h): weight folding/packing at create time and the
 // stream-ordered launch sequence of one SeparationModel.forward (reference model/model.py:402-461).
+//
+// Per forward (B utterances, T frames, 24 blocks):
+//   k_stft -> k_gate -> 24 x [ conv1d GEMM (loader: previous block's residual update)
+//                              -> k_dw_stats -> res_out GEMM (loader: GN1, dconv, PReLU, GN2)
+//                              -> k_att_stats ]
+//   -> k_head_stats -> output GEMM (loader: residual update, PReLU, GN) -> k_vad1 -> k_istft
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -30,8 +38,14 @@ int fail(int code, const std::string& msg) {
       return fail(SEPVAD_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
   } while (0)
 
+// Packed pointwise-conv weight: fp32 [M][K] and the fp16 split of the row-scaled copy.
+struct PackedW {
+  size_t w32 = 0, whi = 0, wlo = 0, scale = 0;
+};
+
 struct BlockOff {
-  size_t w1t, b1, g1, be1, wd, bd, w2t, b2, g2, be2, attp, lna_g, lna_b, lnb_g, lnb_b;
+  PackedW w1, w2;
+  size_t b1, g1, be1, wd, bd, b2, g2, be2, attp, lna_g, lna_b, lnb_g, lnb_b;
   float a1, a2;
   int dil;
 };
@@ -40,9 +54,9 @@ struct Workspace {
   int Bmax = 0, Tpmax = 0;
   char* base = nullptr;
   size_t bytes = 0;
-  float2* X; float* specdb; float* S0; float* O[2]; float* A; float* D; float* R; float* U;
-  float* P; float* masks; float* gain; float* colsum; float* rowsum; float* vad;
-  double* sl_gate; double* sl_g1; double* sl_dw; double* sl_att; double* sl_hp; double* moments;
+  float2* X; float* specdb; float* S0; float* O[2]; float* A; float* R;
+  float* masks; float* colsum; float* rowsum; float* at; float* af; float* vy; float* vad;
+  double* sl_gate; double* sl_g1; double* sl_dw; double* mom; double* sl_hs; double* sl_vad;
 };
 
 }  // namespace
@@ -51,11 +65,14 @@ struct sepvad_model {
   SepVadConfig cfg{};
   int device = 0;
   int nblk = 0;
-  float* dparams = nullptr;  // packed weights (device)
+  int prec = PREC_F16X3;
+  float* dparams = nullptr;   // packed fp32 weights (device)
+  __half* dhalf = nullptr;    // packed fp16 split weights (device)
   std::vector<BlockOff> blk;
   size_t win_in = 0, win_out = 0, win_inv = 0, tw = 0;
   size_t ln_g = 0, ln_b = 0;
-  size_t out_g = 0, out_b = 0, wot = 0, bo = 0;
+  PackedW wout;
+  size_t out_g = 0, out_b = 0, bo = 0;
   float out_a = 0.f;
   size_t v_w1 = 0, v_b1 = 0, v_g = 0, v_b = 0, v_w2 = 0;
   float v_a = 0.f, v_b2 = 0.f;
@@ -69,6 +86,7 @@ struct sepvad_model {
   int gemm_launches = 0, g2_launches = 0;
 
   const float* P(size_t off) const { return dparams + off; }
+  const __half* H(size_t off) const { return dhalf + off; }
 };
 
 namespace {
@@ -89,14 +107,20 @@ struct TensorMap {
 
 struct Packer {
   std::vector<float> blob;
+  std::vector<__half> hblob;
   size_t add(const float* p, size_t n) {
     size_t off = blob.size();
-    // keep every array 16-byte aligned for float4 loads
     blob.insert(blob.end(), p, p + n);
-    while (blob.size() % 4) blob.push_back(0.f);
+    while (blob.size() % 4) blob.push_back(0.f);  // 16-byte aligned arrays (float4 loads)
     return off;
   }
   size_t add(const std::vector<float>& v) { return add(v.data(), v.size()); }
+  size_t addh(const std::vector<__half>& v) {
+    size_t off = hblob.size();
+    hblob.insert(hblob.end(), v.begin(), v.end());
+    while (hblob.size() % 8) hblob.push_back(__float2half_rn(0.f));
+    return off;
+  }
 };
 
 // torch.nn.utils.weight_norm (dim=0): w = v * (g / ||v||_2 over all dims but 0).
@@ -112,12 +136,34 @@ std::vector<float> fold_wn(const float* g, const float* v, int cout, int rest) {
   return w;
 }
 
-// [cout][cin] -> [cin][mpad] (k-major, zero-padded columns)
-std::vector<float> transpose_pad(const std::vector<float>& w, int cout, int cin, int mpad) {
-  std::vector<float> t((size_t)cin * mpad, 0.f);
-  for (int o = 0; o < cout; ++o)
-    for (int i = 0; i < cin; ++i) t[(size_t)i * mpad + o] = w[(size_t)o * cin + i];
-  return t;
+// [cout][cin] fp32 -> zero-padded [mpad][cin] fp32 + the fp16 hi/lo split of each row scaled by
+// 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^e undoes it exactly.
+PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int cin, int mpad) {
+  PackedW p;
+  std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
+  std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin);
+  for (int o = 0; o < mpad; ++o) {
+    float mx = 0.f;
+    if (o < cout)
+      for (int i = 0; i < cin; ++i) mx = std::max(mx, std::fabs(w[(size_t)o * cin + i]));
+    int e = 0;
+    if (mx > 0.f) { (void)std::frexp(mx, &e); }  // mx = f * 2^e, f in [0.5, 1)
+    const float s = std::ldexp(1.f, -e);
+    sc[o] = std::ldexp(1.f, e);
+    for (int i = 0; i < cin; ++i) {
+      const float v = o < cout ? w[(size_t)o * cin + i] : 0.f;
+      w32[(size_t)o * cin + i] = v;
+      const float vs = v * s;
+      const __half hh = __float2half_rn(vs);
+      hi[(size_t)o * cin + i] = hh;
+      lo[(size_t)o * cin + i] = __float2half_rn(vs - __half2float(hh));
+    }
+  }
+  p.w32 = pk.add(w32);
+  p.scale = pk.add(sc);
+  p.whi = pk.addh(hi);
+  p.wlo = pk.addh(lo);
+  return p;
 }
 
 int ws_reserve(sepvad_model* h, int B, int N) {
@@ -129,15 +175,14 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   const size_t bt = (size_t)Bm * Tm;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
-  const size_t oX = take(bt * NBIN * 8), oSpec = take(bt * NBIN * 4), oS0 = take(bt * CH * 4);
-  const size_t oO0 = take(bt * CH * 4), oO1 = take(bt * CH * 4), oA = take(bt * CH * 4);
-  const size_t oD = take(bt * HID * 4), oR = take(bt * CH * 4), oU = take(bt * CH * 4);
-  const size_t oP = take(bt * CH * 4), oM = take(bt * 2 * NBIN * 4), oG = take(bt * 2 * 4);
+  const size_t oX = take(bt * NBIN * 8), oSpec = take(bt * SPEC_LD * 4), oS0 = take(bt * CH * 4);
+  const size_t oO0 = take(bt * CH * 4), oO1 = take(bt * CH * 4), oA = take(bt * CH * 4), oR = take(bt * CH * 4);
+  const size_t oM = take(bt * MOUT_PAD * 4);
   const size_t oCs = take(bt * (CH / TILE) * 4), oRs = take((size_t)Bm * (Tm / TILE) * CH * 4);
-  const size_t oV = take(bt * 2 * 4);
-  const size_t oSg = take((size_t)Bm * gate_tiles() * 16), oS1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
-  const size_t oSd = take((size_t)Bm * 16 * 16), oSa = take((size_t)Bm * 16 * 16), oSh = take((size_t)Bm * 16 * 16);
-  const size_t oMo = take((size_t)Bm * CH * 5 * 8);
+  const size_t oAt = take(bt * 4), oAf = take((size_t)Bm * CH * 4), oVy = take(bt * 2 * 4 * 4), oV = take(bt * 2 * 4);
+  const size_t oSg = take(bt / GATE_ROWS * 16 + 16), oS1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
+  const size_t oSd = take(bt / STAT_ROWS * 16 + 16), oMo = take(bt / STAT_ROWS * NMOM * 8 + 16);
+  const size_t oSh = take(bt / STAT_ROWS * 16 + 16), oSv = take(bt * 2 / VAD_ROWS * 16 + 16);
   char* base = nullptr;
   HIPCHK(hipMalloc(&base, off));
   HIPCHK(hipMemset(base, 0, off));
@@ -145,34 +190,13 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   w.base = base; w.bytes = off; w.Bmax = Bm; w.Tpmax = Tm;
   w.X = (float2*)(base + oX); w.specdb = (float*)(base + oSpec); w.S0 = (float*)(base + oS0);
   w.O[0] = (float*)(base + oO0); w.O[1] = (float*)(base + oO1); w.A = (float*)(base + oA);
-  w.D = (float*)(base + oD); w.R = (float*)(base + oR); w.U = (float*)(base + oU);
-  w.P = (float*)(base + oP); w.masks = (float*)(base + oM); w.gain = (float*)(base + oG);
-  w.colsum = (float*)(base + oCs); w.rowsum = (float*)(base + oRs); w.vad = (float*)(base + oV);
+  w.R = (float*)(base + oR); w.masks = (float*)(base + oM);
+  w.colsum = (float*)(base + oCs); w.rowsum = (float*)(base + oRs); w.at = (float*)(base + oAt);
+  w.af = (float*)(base + oAf); w.vy = (float*)(base + oVy); w.vad = (float*)(base + oV);
   w.sl_gate = (double*)(base + oSg); w.sl_g1 = (double*)(base + oS1); w.sl_dw = (double*)(base + oSd);
-  w.sl_att = (double*)(base + oSa); w.sl_hp = (double*)(base + oSh); w.moments = (double*)(base + oMo);
+  w.mom = (double*)(base + oMo); w.sl_hs = (double*)(base + oSh); w.sl_vad = (double*)(base + oSv);
   return SEPVAD_OK;
 }
-
-// The loader transform that turns (o_{i}, u_{i}) of block i into the next block input o_{i+1}.
-LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float* U) {
-  LoadSpec ld{};
-  ld.X = O; ld.X2 = U;
-  const BlockOff& bo = h->blk[i];
-  if (h->cfg.ln_mode == SEPVAD_LN_RECURSIVE) {
-    ld.mode = LD_RECURSIVE;
-    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
-    ld.g2 = h->P(bo.lnb_g); ld.be2 = h->P(bo.lnb_b); ld.eps2 = 1e-5f;
-    ld.moments = h->ws.moments;
-  } else if (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL) {
-    ld.mode = LD_RESIDUAL;
-    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
-    ld.slots = h->ws.sl_att; ld.nslots = CH / 16;
-  } else {
-    ld.mode = LD_ADD;
-  }
-  return ld;
-}
-
 
 // Restores the caller's current HIP device on scope exit (torch shares this runtime).
 struct DeviceGuard {
@@ -196,6 +220,35 @@ int ev_record(sepvad_model* h, hipStream_t s) {
   return 0;
 }
 
+void set_weights(const sepvad_model* h, GemmArgs& g, const PackedW& w) {
+  g.prec = h->prec;
+  g.W32 = h->P(w.w32);
+  g.Whi = h->H(w.whi);
+  g.Wlo = h->H(w.wlo);
+  g.wscale = h->P(w.scale);
+}
+
+// The residual-stream transform that turns (o_i, r_i) of block i into the next block input.
+LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float* R, int Tp) {
+  LoadSpec ld{};
+  ld.X = O; ld.X2 = R;
+  if (h->cfg.tf_attention) { ld.at = h->ws.at; ld.af = h->ws.af; }
+  const BlockOff& bo = h->blk[i];
+  if (h->cfg.ln_mode == SEPVAD_LN_RECURSIVE) {
+    ld.mode = LD_RECURSIVE;
+    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
+    ld.g2 = h->P(bo.lnb_g); ld.be2 = h->P(bo.lnb_b); ld.eps2 = 1e-5f;
+    ld.slots = h->ws.mom; ld.nslots = Tp / STAT_ROWS; ld.sstride = NMOM;
+  } else if (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL) {
+    ld.mode = LD_RESIDUAL;
+    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
+    ld.slots = h->ws.mom + 2; ld.nslots = Tp / STAT_ROWS; ld.sstride = NMOM;  // (Σr', Σr'²) at 2, 3
+  } else {
+    ld.mode = LD_ADD;
+  }
+  return ld;
+}
+
 }  // namespace
 
 extern "C" {
@@ -207,9 +260,9 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
                             const int64_t* numels, int32_t n, int32_t device) {
   if (!cfg || !tensors || !names || !numels) { g_err = "null argument"; return nullptr; }
   const SepVadConfig& c = *cfg;
-  if (c.n_fft != NFFT || c.bn_dim != CH || c.h_dim != HID || c.num_spk != 2 || c.precision != SEPVAD_PREC_FP32 ||
-      c.layer < 1 || c.stack < 1) {
-    g_err = "unsupported configuration (native path: n_fft=512, BN_dim=256, H_dim=512, num_spk=2, fp32)";
+  if (c.n_fft != NFFT || c.bn_dim != CH || c.h_dim != HID || c.num_spk != 2 || c.layer < 1 || c.stack < 1 ||
+      (c.precision != SEPVAD_PREC_FP32 && c.precision != SEPVAD_PREC_F16X3)) {
+    g_err = "unsupported configuration (native path: n_fft=512, BN_dim=256, H_dim=512, num_spk=2)";
     return nullptr;
   }
   int ndev = 0;
@@ -221,6 +274,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
   h->cfg = c;
   h->device = device;
   h->nblk = c.layer * c.stack;
+  h->prec = c.precision == SEPVAD_PREC_FP32 ? PREC_F32 : PREC_F16X3;
   Packer pk;
   bool ok = true;
   auto get = [&](const std::string& k, int64_t numel) -> const float* {
@@ -228,11 +282,12 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     if (!p) ok = false;
     return p;
   };
+#define BAIL() do { if (!ok) { delete h; return nullptr; } } while (0)
   // windows (model/model.py:383-387) and FFT twiddles
   const float* wi = get("spec_input.spec.window", NFFT);
   const float* wo = get("spec_output.window", NFFT);
   const float* wv = get("inv_spec.window", NFFT);
-  if (!ok) { delete h; return nullptr; }
+  BAIL();
   h->win_in = pk.add(wi, NFFT);
   h->win_out = pk.add(wo, NFFT);
   h->win_inv = pk.add(wv, NFFT);
@@ -246,9 +301,13 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     }
     h->tw = pk.add(tw);
   }
-  h->ln_g = pk.add(get("TCN.LN.weight", CH), CH);
-  h->ln_b = pk.add(get("TCN.LN.bias", CH), CH);
-  if (!ok) { delete h; return nullptr; }
+  {
+    const float* lg = get("TCN.LN.weight", CH);
+    const float* lb = get("TCN.LN.bias", CH);
+    BAIL();
+    h->ln_g = pk.add(lg, CH);
+    h->ln_b = pk.add(lb, CH);
+  }
   // blocks (model/model.py:285-295,103-127,182-195,310-319)
   for (int i = 0; i < h->nblk; ++i) {
     BlockOff bo{};
@@ -268,14 +327,14 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const float* r1b = get(p + ".reg1.bias", CH);
     const float* r2g = get(p + ".reg2.weight", HID);
     const float* r2b = get(p + ".reg2.bias", HID);
-    if (!ok) { delete h; return nullptr; }
-    bo.w1t = pk.add(transpose_pad(fold_wn(g1, v1, CH, CH), CH, CH, CH));
+    BAIL();
+    bo.w1 = pack_pointwise(pk, fold_wn(g1, v1, CH, CH), CH, CH, CH);
     bo.b1 = pk.add(b1, CH);
     bo.g1 = pk.add(r1g, CH);
     bo.be1 = pk.add(r1b, CH);
     bo.wd = pk.add(fold_wn(gd, vd, HID, 3));
     bo.bd = pk.add(bd, HID);
-    bo.w2t = pk.add(transpose_pad(fold_wn(g2, v2, CH, HID), CH, HID, CH));
+    bo.w2 = pack_pointwise(pk, fold_wn(g2, v2, CH, HID), CH, HID, CH);
     bo.b2 = pk.add(b2, CH);
     bo.g2 = pk.add(r2g, HID);
     bo.be2 = pk.add(r2b, HID);
@@ -290,25 +349,29 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       for (int j = 0; j < 4; ++j) {
         const float* w = get(q + convs[j] + ".weight", 3);
         const float* bb = get(q + convs[j] + ".bias", 1);
-        if (!ok) { delete h; return nullptr; }
+        BAIL();
         attp[4 * j + 0] = w[0]; attp[4 * j + 1] = w[1]; attp[4 * j + 2] = w[2]; attp[4 * j + 3] = bb[0];
       }
       const float* pt = get(q + ".prelu_t.weight", 1);
       const float* pf = get(q + ".prelu_f.weight", 1);
-      if (!ok) { delete h; return nullptr; }
+      BAIL();
       attp[16] = pt[0]; attp[17] = pf[0];
     }
     bo.attp = pk.add(attp);
     if (c.ln_mode == SEPVAD_LN_RECURSIVE) {
-      bo.lna_g = pk.add(get("TCN.ln_first_modules." + std::to_string(i) + ".weight", CH), CH);
-      bo.lna_b = pk.add(get("TCN.ln_first_modules." + std::to_string(i) + ".bias", CH), CH);
-      bo.lnb_g = pk.add(get("TCN.ln_second_modules." + std::to_string(i) + ".weight", CH), CH);
-      bo.lnb_b = pk.add(get("TCN.ln_second_modules." + std::to_string(i) + ".bias", CH), CH);
+      const float* fa = get("TCN.ln_first_modules." + std::to_string(i) + ".weight", CH);
+      const float* fb = get("TCN.ln_first_modules." + std::to_string(i) + ".bias", CH);
+      const float* sa = get("TCN.ln_second_modules." + std::to_string(i) + ".weight", CH);
+      const float* sb = get("TCN.ln_second_modules." + std::to_string(i) + ".bias", CH);
+      BAIL();
+      bo.lna_g = pk.add(fa, CH); bo.lna_b = pk.add(fb, CH);
+      bo.lnb_g = pk.add(sa, CH); bo.lnb_b = pk.add(sb, CH);
     } else if (c.ln_mode == SEPVAD_LN_RESIDUAL) {
-      bo.lna_g = pk.add(get("TCN.ln_modules." + std::to_string(i) + ".weight", CH), CH);
-      bo.lna_b = pk.add(get("TCN.ln_modules." + std::to_string(i) + ".bias", CH), CH);
+      const float* fa = get("TCN.ln_modules." + std::to_string(i) + ".weight", CH);
+      const float* fb = get("TCN.ln_modules." + std::to_string(i) + ".bias", CH);
+      BAIL();
+      bo.lna_g = pk.add(fa, CH); bo.lna_b = pk.add(fb, CH);
     }
-    if (!ok) { delete h; return nullptr; }
     h->blk.push_back(bo);
   }
   // output head (model/model.py:322-325)
@@ -316,16 +379,16 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const float* oa = get("TCN.output.0.weight", 1);
     const float* og = get("TCN.output.1.weight", CH);
     const float* ob = get("TCN.output.1.bias", CH);
-    const float* gg = get("TCN.output.2.weight_g", 2 * NBIN);
-    const float* vv = get("TCN.output.2.weight_v", (int64_t)2 * NBIN * CH);
-    const float* bb = get("TCN.output.2.bias", 2 * NBIN);
-    if (!ok) { delete h; return nullptr; }
+    const float* gg = get("TCN.output.2.weight_g", MOUT);
+    const float* vv = get("TCN.output.2.weight_v", (int64_t)MOUT * CH);
+    const float* bb = get("TCN.output.2.bias", MOUT);
+    BAIL();
     h->out_a = oa[0];
     h->out_g = pk.add(og, CH);
     h->out_b = pk.add(ob, CH);
-    h->wot = pk.add(transpose_pad(fold_wn(gg, vv, 2 * NBIN, CH), 2 * NBIN, CH, MOUT_PAD));
+    h->wout = pack_pointwise(pk, fold_wn(gg, vv, MOUT, CH), MOUT, CH, MOUT_PAD);
     std::vector<float> bpad(MOUT_PAD, 0.f);
-    std::memcpy(bpad.data(), bb, 2 * NBIN * sizeof(float));
+    std::memcpy(bpad.data(), bb, MOUT * sizeof(float));
     h->bo = pk.add(bpad);
   }
   // VAD head (model/model.py:153-171)
@@ -339,7 +402,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const float* g2 = get("vad.output_layer_vad.weight_g", 1);
     const float* v2 = get("vad.output_layer_vad.weight_v", 12);
     const float* b2 = get("vad.output_layer_vad.bias", 1);
-    if (!ok) { delete h; return nullptr; }
+    BAIL();
     h->v_w1 = pk.add(fold_wn(g1, v1, 4, NBIN * 5));
     h->v_b1 = pk.add(b1, 4);
     h->v_a = a[0];
@@ -355,15 +418,18 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       const float* w = get("activity_input.weight", 9);
       const float* bb = get("activity_input.bias", 1);
       const float* pa = get("prelu.weight", 1);
-      if (!ok) { delete h; return nullptr; }
+      BAIL();
       std::memcpy(gw.data(), w, 9 * sizeof(float));
       gw[9] = bb[0];
       gw[10] = pa[0];
     }
     h->gate = pk.add(gw);
   }
+#undef BAIL
   if (hipMalloc(&h->dparams, pk.blob.size() * sizeof(float)) != hipSuccess ||
-      hipMemcpy(h->dparams, pk.blob.data(), pk.blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(h->dparams, pk.blob.data(), pk.blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&h->dhalf, pk.hblob.size() * sizeof(__half)) != hipSuccess ||
+      hipMemcpy(h->dhalf, pk.hblob.data(), pk.hblob.size() * sizeof(__half), hipMemcpyHostToDevice) != hipSuccess) {
     g_err = "device allocation/upload of the packed weights failed";
     delete h;
     return nullptr;
@@ -375,6 +441,14 @@ int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N) {
   if (!h || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_reserve: bad arguments");
   DeviceGuard dg(h->device);
   return ws_reserve(h, B, N);
+}
+
+int32_t sepvad_set_precision(sepvad_handle h, int32_t precision) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  if (precision == SEPVAD_PREC_FP32) h->prec = PREC_F32;
+  else if (precision == SEPVAD_PREC_F16X3) h->prec = PREC_F16X3;
+  else return fail(SEPVAD_E_ARG, "unknown precision");
+  return SEPVAD_OK;
 }
 
 int32_t sepvad_set_timing(sepvad_handle h, int32_t on) {
@@ -398,8 +472,6 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
   if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
-  if (Tp > 1024) return fail(SEPVAD_E_SHAPE, "sepvad_forward: at most 1023 STFT frames (N < 261888) per call; "
-                                             "use the streaming wrapper for longer inputs");
   DeviceGuard dg(h->device);
   int rc = ws_reserve(h, B, N);
   if (rc) return rc;
@@ -436,19 +508,21 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     HIPCHK(launch_gate(ga, s));
   }
   // 3. TCN blocks
-  int cur = 0;  // w.O[cur] holds the current block input o after G1 materializes it
+  int cur = 0;  // w.O[cur] holds the current block input o once the conv1d GEMM materialized it
+  const int nsl_g1 = ntu * (CH / TILE);
   for (int i = 0; i < h->nblk; ++i) {
     const BlockOff& bo = h->blk[i];
     const int nxt = (i == 0) ? 0 : (cur ^ 1);
     GemmArgs g{};
-    g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH;
-    g.WT = h->P(bo.w1t); g.bias = h->P(bo.b1); g.prelu = bo.a1;
+    g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH; g.ldy = CH;
+    set_weights(h, g, bo.w1);
+    g.bias = h->P(bo.b1); g.prelu = bo.a1;
     if (i == 0) {
       g.ld.mode = LD_GN; g.ld.X = w.S0;
       g.ld.g1 = h->P(h->ln_g); g.ld.be1 = h->P(h->ln_b); g.ld.eps1 = 1e-8f;
-      g.ld.slots = w.sl_gate; g.ld.nslots = gate_tiles();
+      g.ld.slots = w.sl_gate; g.ld.nslots = Tp / GATE_ROWS; g.ld.sstride = 2;
     } else {
-      g.ld = residual_spec(h, i - 1, w.O[cur], w.U);
+      g.ld = residual_spec(h, i - 1, w.O[cur], w.R, Tp);
     }
     g.Xmat = w.O[nxt];
     g.Y = w.A; g.out_slots = w.sl_g1;
@@ -458,18 +532,22 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     gemm_ev.push_back((int)h->ev.size() - 2);
     cur = nxt;
 
-    DwArgs d{};
+    DwStatsArgs d{};
     d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
-    d.slots = w.sl_g1; d.nslots = (CH / TILE) * ntu;
+    d.slots = w.sl_g1; d.nslots = nsl_g1;
     d.g1 = h->P(bo.g1); d.be1 = h->P(bo.be1); d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
-    d.D = w.D; d.out_slots = w.sl_dw;
-    HIPCHK(launch_dw(d, s));
+    d.out_slots = w.sl_dw;
+    HIPCHK(launch_dw_stats(d, s));
 
     GemmArgs g2{};
-    g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID;
-    g2.WT = h->P(bo.w2t); g2.bias = h->P(bo.b2);
-    g2.ld.mode = LD_GN; g2.ld.X = w.D; g2.ld.g1 = h->P(bo.g2); g2.ld.be1 = h->P(bo.be2); g2.ld.eps1 = 1e-8f;
-    g2.ld.slots = w.sl_dw; g2.ld.nslots = CH / 16;
+    g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
+    set_weights(h, g2, bo.w2);
+    g2.bias = h->P(bo.b2);
+    g2.ld.mode = LD_DW; g2.ld.X = w.A;
+    g2.ld.g1 = h->P(bo.g2); g2.ld.be1 = h->P(bo.be2); g2.ld.eps1 = 1e-8f;
+    g2.ld.slots = w.sl_dw; g2.ld.nslots = Tp / STAT_ROWS; g2.ld.sstride = 2;
+    g2.ld.wd = h->P(bo.wd); g2.ld.bd = h->P(bo.bd); g2.ld.alpha_d = bo.a2; g2.ld.dil = bo.dil;
+    g2.ld.gd1 = h->P(bo.g1); g2.ld.bed1 = h->P(bo.be1); g2.ld.slots_d1 = w.sl_g1; g2.ld.nslots_d1 = nsl_g1;
     g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
@@ -477,54 +555,62 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     gemm_ev.push_back((int)h->ev.size() - 2);
     g2_ev.push_back((int)h->ev.size() - 2);
 
-    AttArgs at{};
+    AttStatsArgs at{};
     at.B = B; at.T = T; at.Tp = Tp; at.mtiles = CH / TILE; at.ntiles = ntu; at.tf_att = c.tf_attention;
     at.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     at.R = w.R; at.O = w.O[cur]; at.colsum = w.colsum; at.rowsum = w.rowsum; at.attp = h->P(bo.attp);
-    at.U = w.U; at.moments = w.moments; at.out_slots = w.sl_att;
-    HIPCHK(launch_att(at, s));
+    if (c.ln_mode == SEPVAD_LN_RECURSIVE) { at.ga = h->P(bo.lna_g); at.bea = h->P(bo.lna_b); }
+    at.at = w.at; at.af = w.af; at.out_mom = w.mom;
+    HIPCHK(launch_att_stats(at, s));
   }
   // 4. output head: PReLU -> GN(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
   {
-    HeadPrepArgs hp{};
-    hp.B = B; hp.T = T; hp.Tp = Tp;
-    hp.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.U);
-    hp.alpha = h->out_a; hp.P = w.P; hp.out_slots = w.sl_hp;
-    HIPCHK(launch_head_prep(hp, s));
+    HeadStatsArgs hs{};
+    hs.B = B; hs.T = T; hs.Tp = Tp;
+    hs.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
+    hs.ld.alpha_h = h->out_a;
+    hs.out_slots = w.sl_hs;
+    HIPCHK(launch_head_stats(hs, s));
     GemmArgs g{};
-    g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = 2 * NBIN; g.K = CH;
-    g.WT = h->P(h->wot); g.bias = h->P(h->bo);
-    g.ld.mode = LD_GN; g.ld.X = w.P; g.ld.g1 = h->P(h->out_g); g.ld.be1 = h->P(h->out_b); g.ld.eps1 = 1e-5f;
-    g.ld.slots = w.sl_hp; g.ld.nslots = CH / 16;
+    g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
+    set_weights(h, g, h->wout);
+    g.bias = h->P(h->bo);
+    g.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
+    g.ld.head = 1; g.ld.alpha_h = h->out_a; g.ld.gh = h->P(h->out_g); g.ld.beh = h->P(h->out_b);
+    g.ld.epsh = 1e-5f; g.ld.slots_h = w.sl_hs; g.ld.nslots_h = Tp / STAT_ROWS;
     g.Y = w.masks; g.Yside = out->masks_b;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     gemm_ev.push_back((int)h->ev.size() - 2);
   }
-  // 5. VAD head + inference-only smoothing (model/model.py:424-427,434-436,444-457)
+  // 5. VAD conv1_1 (model/model.py:424-427,434-436)
   const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
   const bool kw_on = kw && kw->enabled && c.final_vad;
   if (has_vad) {
-    VadArgs v{};
-    v.B = B; v.T = T; v.Tp = Tp; v.masked_speakers = c.final_vad_masked_speakers; v.noisy_phase = c.noisy_phase;
+    Vad1Args v{};
+    v.B = B; v.T = T; v.Tp = Tp; v.masked_speakers = c.final_vad_masked_speakers;
     v.masks = w.masks; v.X = w.X;
-    v.w1 = h->P(h->v_w1); v.b1 = h->P(h->v_b1); v.alpha = h->v_a; v.g = h->P(h->v_g); v.be = h->P(h->v_b);
-    v.w2 = h->P(h->v_w2); v.b2 = h->v_b2;
-    v.kw_enabled = kw_on;
-    v.filt = kw_on && (kw->filter_signals_by_smo_vad || kw->filter_signals_by_unsmo_vad);
-    v.ret_smooth = kw_on && kw->return_smoothed_vad;
-    v.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
-    v.vad_out = out->vad ? out->vad : w.vad;
-    v.gain = w.gain;
-    HIPCHK(launch_vad(v, s));
+    v.w1 = h->P(h->v_w1); v.b1 = h->P(h->v_b1); v.alpha = h->v_a;
+    v.vy = w.vy; v.out_slots = w.sl_vad;
+    HIPCHK(launch_vad1(v, s));
   }
-  // 6. est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-439,452-455,460)
+  // 6. VAD tail + est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-460)
   {
     IstftArgs is{};
-    is.BS = B * 2; is.S = 2; is.N = N; is.T = T; is.Tp = Tp; is.noisy_phase = c.noisy_phase; is.est_mode = 1;
-    is.X = w.X; is.masks = w.masks; is.gain = (has_vad && kw_on) ? w.gain : nullptr;
+    is.BS = B * 2; is.S = 2; is.N = N; is.T = T; is.Tp = Tp; is.est_mode = 1;
+    is.X = w.X; is.masks = w.masks;
     is.window = h->P(h->win_inv); is.tw = (const float2*)h->P(h->tw);
+    is.has_vad = has_vad;
+    if (has_vad) {
+      is.kw_enabled = kw_on;
+      is.filt = kw_on && (kw->filter_signals_by_smo_vad || kw->filter_signals_by_unsmo_vad);
+      is.ret_smooth = kw_on && kw->return_smoothed_vad;
+      is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
+      is.vy = w.vy; is.vslots = w.sl_vad; is.nvslots = Tp / VAD_ROWS;
+      is.vg = h->P(h->v_g); is.vbe = h->P(h->v_b); is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
+      is.vad_out = out->vad ? out->vad : w.vad;
+    }
     is.est_out = (float2*)out->est; is.mask_out = out->mask; is.y = out->sep;
     HIPCHK(launch_istft(is, s));
   }
@@ -575,6 +661,7 @@ void sepvad_destroy(sepvad_handle h) {
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   if (h->ws.base) (void)hipFree(h->ws.base);
   if (h->dparams) (void)hipFree(h->dparams);
+  if (h->dhalf) (void)hipFree(h->dhalf);
   delete h;
 }
 

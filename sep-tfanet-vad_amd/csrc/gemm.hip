@@ -1,0 +1,400 @@
+// Pointwise (1x1 conv) GEMMs of the TCN, channel-last:  Y[t][m] = sum_k X'[t][k] * W[m][k] + bias[m]
+//   DepthConv1d.conv1d  256->256  (reference model/model.py:104,132)   EP_PRELU_STATS
+//   DepthConv1d.res_out 512->256  (model/model.py:114,144)             EP_BIAS_ATT, A operand LD_DW
+//   TCN.output.2        256->514  (model/model.py:324,357)             EP_BIAS_OUT, A operand + head
+// X' is produced while staging (normalize-on-load): the residual-stream update of the previous
+// block (recursive / residual LN with the TF-attention gates folded in), the depthwise dilated
+// conv + both GroupNorms for res_out, or PReLU + GroupNorm for the output head. None of those
+// tensors is ever materialized except the block input o (written once, by m-tile 0).
+//
+// Arithmetic (GemmArgs::prec):
+//   PREC_F16X3: fp32-equivalent GEMM on fp16 MFMA. x = x_hi + x_lo with x_hi = fp16(x),
+//               x_lo = fp16(x - x_hi) (weights pre-scaled per row by 2^-e into [0.5,1));
+//               acc += A_hi B_hi + A_hi B_lo + A_lo B_hi  on v_mfma_f32_32x32x16_f16, fp32 accumulate.
+//               Products of fp16 are exact in fp32, so only the dropped lo*lo term (~2^-22 relative)
+//               and fp32 accumulation remain: parity matches the fp32 path (tests/test_gpu_parity.py).
+//   PREC_F32:   v_mfma_f32_32x32x2_f32 (exact fp32 fma chain), 1/16 of the f16 MFMA rate.
+// Tile 64 frames x 64 channels, K chunk 32, 4 waves (2x2), one 32x32 accumulator per wave;
+// register-staged double-buffered LDS, one barrier per K chunk.
+#include "device_common.h"
+
+namespace sepvad {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BT = 64;        // frames per tile
+constexpr int BMC = 64;       // output channels per tile
+constexpr int BK = 32;        // K chunk
+constexpr int LDH = BK + 8;   // halves per LDS row: 80 B rows make the 16-B fragment reads conflict-free
+constexpr int LDF = BK + 1;   // floats per LDS row (fp32 path)
+constexpr int KMAX = 512;
+constexpr int DWROWS = BT + 8;  // LD_DW halo rows (dilation <= 4)
+
+struct SmemF16 {
+  __half Ahi[2][BT][LDH], Alo[2][BT][LDH], Bhi[2][BMC][LDH], Blo[2][BMC][LDH];
+};
+struct SmemF32 {
+  float A[2][BT][LDF], B[2][BMC][LDF];
+};
+
+__device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
+  const __half h0 = __float2half_rn(v.x), h1 = __float2half_rn(v.y), h2 = __float2half_rn(v.z),
+               h3 = __float2half_rn(v.w);
+  const __half l0 = __float2half_rn(v.x - __half2float(h0)), l1 = __float2half_rn(v.y - __half2float(h1)),
+               l2 = __float2half_rn(v.z - __half2float(h2)), l3 = __float2half_rn(v.w - __half2float(h3));
+  __half2 a = __halves2half2(h0, h1), b = __halves2half2(h2, h3);
+  __half2 c = __halves2half2(l0, l1), d = __halves2half2(l2, l3);
+  hi = make_uint2(*reinterpret_cast<unsigned*>(&a), *reinterpret_cast<unsigned*>(&b));
+  lo = make_uint2(*reinterpret_cast<unsigned*>(&c), *reinterpret_cast<unsigned*>(&d));
+}
+
+template <int PREC, int LM, int HEAD, int EP>
+__global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
+  using Smem = typename std::conditional<PREC == PREC_F16X3, SmemF16, SmemF32>::type;
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  constexpr bool NEED_C = (LM == LD_GN || LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_DW);
+  __shared__ float cf[4][NEED_C ? KMAX : 1];       // resid coefs / (LD_DW: s2,h2 over 512; s1,h1 over 256)
+  __shared__ float hco[2][HEAD ? CH : 1];          // head GN_out affine
+  __shared__ float afk[(LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) ? KMAX : 1];
+  __shared__ float atr[BT];
+  __shared__ float wdl[LM == LD_DW ? HID * 4 : 1];  // dconv taps (3) + bias per output channel
+  __shared__ float Hs[LM == LD_DW ? DWROWS : 1][LM == LD_DW ? 17 : 1];
+  __shared__ double red[16];
+  __shared__ float bc[4];
+  __shared__ float epi[2][2][64];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntu = a.Tp / BT;
+  const int b = blockIdx.x / ntu, rt = blockIdx.x % ntu;
+  const int t0 = rt * BT;
+  const int mt = blockIdx.y, m0 = mt * BMC;
+  const int K = a.K, T = a.T, Tp = a.Tp;
+  const LoadSpec& ld = a.ld;
+
+  // ---------------- prologue: per-utterance coefficients in LDS ----------------
+  if constexpr (LM == LD_GN || LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
+    resid_coefs(ld, b, K, T, cf[0], cf[1], cf[2], cf[3], red, bc);
+  }
+  if constexpr (LM == LD_DW) {
+    // GN1 over a (CH channels, stats from the conv1d epilogue), GN2 over d (HID channels)
+    gn_coefs(ld.slots_d1 + (size_t)b * ld.nslots_d1 * 2, ld.nslots_d1, 2, (double)CH * T, 1e-8f, ld.gd1,
+             ld.bed1, CH, cf[2], cf[3], bc);
+    gn_coefs(ld.slots + (size_t)b * ld.nslots * ld.sstride, ld.nslots, ld.sstride, (double)HID * T, ld.eps1,
+             ld.g1, ld.be1, HID, cf[0], cf[1], bc);
+    for (int j = tid; j < HID; j += 256) {
+      wdl[j * 4 + 0] = ld.wd[j * 3 + 0];
+      wdl[j * 4 + 1] = ld.wd[j * 3 + 1];
+      wdl[j * 4 + 2] = ld.wd[j * 3 + 2];
+      wdl[j * 4 + 3] = ld.bd[j];
+    }
+  }
+  if constexpr (HEAD) {
+    gn_coefs(ld.slots_h + (size_t)b * ld.nslots_h * 2, ld.nslots_h, 2, (double)K * T, ld.epsh, ld.gh, ld.beh, K,
+             hco[0], hco[1], bc);
+  }
+  if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
+    for (int k = tid; k < K; k += 256) afk[k] = ld.af ? ld.af[(size_t)b * K + k] : 1.f;
+    if (tid < BT) atr[tid] = ld.at ? ld.at[(size_t)b * Tp + t0 + tid] : 1.f;
+  }
+  __syncthreads();
+
+  // ---------------- staging: global -> registers -> (transform) -> LDS ----------------
+  float4 ro[2], rr[2];
+  uint4 whr, wlr;
+  float4 wf[2];
+  const size_t arow0 = (size_t)b * Tp + t0;
+
+  auto gather = [&](int k0) {
+    if constexpr (LM == LD_DW) {
+      const int c0 = k0 >> 1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 2, q = idx & 3;
+        const int t = t0 - ld.dil + row;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < BT + 2 * ld.dil && t >= 0 && t < T)
+          v = *reinterpret_cast<const float4*>(ld.X + ((size_t)b * Tp + t) * CH + c0 + 4 * q);
+        ro[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        const size_t off = (arow0 + row) * K + k0 + c4;
+        ro[i] = *reinterpret_cast<const float4*>(ld.X + off);
+        if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD)
+          rr[i] = *reinterpret_cast<const float4*>(ld.X2 + off);
+      }
+    }
+    if constexpr (PREC == PREC_F16X3) {
+      const int row = tid >> 2, q = tid & 3;
+      whr = *reinterpret_cast<const uint4*>(a.Whi + (size_t)(m0 + row) * K + k0 + 8 * q);
+      wlr = *reinterpret_cast<const uint4*>(a.Wlo + (size_t)(m0 + row) * K + k0 + 8 * q);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        wf[i] = *reinterpret_cast<const float4*>(a.W32 + (size_t)(m0 + row) * K + k0 + c4);
+      }
+    }
+  };
+
+  auto put_a = [&](int buf, int row, int col, const float4& v) {  // 4 consecutive k at (row, col)
+    if constexpr (PREC == PREC_F16X3) {
+      uint2 hi, lo;
+      split4(v, hi, lo);
+      *reinterpret_cast<uint2*>(&sm.Ahi[buf][row][col]) = hi;
+      *reinterpret_cast<uint2*>(&sm.Alo[buf][row][col]) = lo;
+    } else {
+      sm.A[buf][row][col + 0] = v.x; sm.A[buf][row][col + 1] = v.y;
+      sm.A[buf][row][col + 2] = v.z; sm.A[buf][row][col + 3] = v.w;
+    }
+  };
+
+  auto head_apply = [&](float x, int k) -> float {
+    if constexpr (HEAD) return fmaf(prelu_f(x, ld.alpha_h), hco[0][k], hco[1][k]);
+    else return x;
+  };
+
+  auto stage = [&](int buf, int k0) {
+    if constexpr (LM == LD_DW) {
+      // 1) normalized a (GN1) of the halo rows into Hs[row][c_local], zero outside [0, T)
+      const int c0 = k0 >> 1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 2, q = idx & 3;
+        if (row < BT + 2 * ld.dil) {
+          const int t = t0 - ld.dil + row;
+          const bool ok = t >= 0 && t < T;
+          const int c = c0 + 4 * q;
+          const float4 v = ro[i];
+          Hs[row][4 * q + 0] = ok ? fmaf(v.x, cf[2][c + 0], cf[3][c + 0]) : 0.f;
+          Hs[row][4 * q + 1] = ok ? fmaf(v.y, cf[2][c + 1], cf[3][c + 1]) : 0.f;
+          Hs[row][4 * q + 2] = ok ? fmaf(v.z, cf[2][c + 2], cf[3][c + 2]) : 0.f;
+          Hs[row][4 * q + 3] = ok ? fmaf(v.w, cf[2][c + 3], cf[3][c + 3]) : 0.f;
+        }
+      }
+      __syncthreads();
+      // 2) d = PReLU(dconv) for 64 rows x 32 output channels, then GN2 -> A tile
+      const int row = tid >> 2, jg = (tid & 3) * 8;
+      const int dl = ld.dil;
+      float dv[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int jl = jg + jj, j = k0 + jl, cl = jl >> 1;
+        const float* w = &wdl[j * 4];
+        float v = w[3];
+        v = fmaf(w[0], Hs[row][cl], v);
+        v = fmaf(w[1], Hs[row + dl][cl], v);
+        v = fmaf(w[2], Hs[row + 2 * dl][cl], v);
+        v = prelu_f(v, ld.alpha_d);
+        dv[jj] = fmaf(v, cf[0][j], cf[1][j]);
+      }
+      put_a(buf, row, jg, make_float4(dv[0], dv[1], dv[2], dv[3]));
+      put_a(buf, row, jg + 4, make_float4(dv[4], dv[5], dv[6], dv[7]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        const int k = k0 + c4;
+        float4 v = ro[i];
+        if constexpr (LM != LD_PLAIN) {
+          float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+          float g0 = 1.f, g1 = 1.f, g2 = 1.f, g3 = 1.f;
+          if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
+            r = rr[i];
+            const float at = atr[row];
+            g0 = afk[k] * at; g1 = afk[k + 1] * at; g2 = afk[k + 2] * at; g3 = afk[k + 3] * at;
+          }
+          v.x = resid_apply<LM>(v.x, r.x, g0, k + 0, cf[0], cf[1], cf[2], cf[3]);
+          v.y = resid_apply<LM>(v.y, r.y, g1, k + 1, cf[0], cf[1], cf[2], cf[3]);
+          v.z = resid_apply<LM>(v.z, r.z, g2, k + 2, cf[0], cf[1], cf[2], cf[3]);
+          v.w = resid_apply<LM>(v.w, r.w, g3, k + 3, cf[0], cf[1], cf[2], cf[3]);
+        }
+        if (a.Xmat != nullptr && mt == 0)
+          *reinterpret_cast<float4*>(a.Xmat + (arow0 + row) * K + k) = v;
+        if constexpr (HEAD) {
+          v.x = head_apply(v.x, k); v.y = head_apply(v.y, k + 1);
+          v.z = head_apply(v.z, k + 2); v.w = head_apply(v.w, k + 3);
+        }
+        put_a(buf, row, c4, v);
+      }
+    }
+    if constexpr (PREC == PREC_F16X3) {
+      const int row = tid >> 2, q = tid & 3;
+      *reinterpret_cast<uint4*>(&sm.Bhi[buf][row][8 * q]) = whr;
+      *reinterpret_cast<uint4*>(&sm.Blo[buf][row][8 * q]) = wlr;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        sm.B[buf][row][c4 + 0] = wf[i].x; sm.B[buf][row][c4 + 1] = wf[i].y;
+        sm.B[buf][row][c4 + 2] = wf[i].z; sm.B[buf][row][c4 + 3] = wf[i].w;
+      }
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+  const int nk = K / BK;
+  gather(0);
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gather((kt + 1) * BK);
+    if constexpr (PREC == PREC_F16X3) {
+      const int ar = wr * 32 + (lane & 31), br = wc * 32 + (lane & 31), kh = 8 * (lane >> 5);
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        const half8 ah = *reinterpret_cast<const half8*>(&sm.Ahi[buf][ar][16 * s + kh]);
+        const half8 al = *reinterpret_cast<const half8*>(&sm.Alo[buf][ar][16 * s + kh]);
+        const half8 bh = *reinterpret_cast<const half8*>(&sm.Bhi[buf][br][16 * s + kh]);
+        const half8 bl = *reinterpret_cast<const half8*>(&sm.Blo[buf][br][16 * s + kh]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+      }
+    } else {
+      const float* Ab = &sm.A[buf][wr * 32 + (lane & 31)][lane >> 5];
+      const float* Bb = &sm.B[buf][wc * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ab[kk], Bb[kk], acc, 0, 0, 0);
+    }
+    if (kt + 1 < nk) stage(buf ^ 1, (kt + 1) * BK);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: lane = column m, registers = rows t ----------------
+  const int col = lane & 31, half = lane >> 5;
+  const int m = m0 + wc * 32 + col;
+  const float ws = (PREC == PREC_F16X3) ? a.wscale[m] : 1.f;
+  const float bias = a.bias[m];
+  auto trow = [&](int r) { return t0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * half; };
+
+  if constexpr (EP == EP_PRELU_STATS) {
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = trow(r);
+      const float v = prelu_f(fmaf(acc[r], ws, bias), a.prelu);
+      a.Y[((size_t)b * Tp + t) * a.ldy + m] = v;
+      if (t < T) { s += v; ss += v * v; }
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    if (lane == 0) { epi[0][0][wave] = s; epi[0][1][wave] = ss; }
+    __syncthreads();
+    if (tid == 0) {
+      double S = 0.0, SS = 0.0;
+      for (int w = 0; w < 4; ++w) { S += epi[0][0][w]; SS += epi[0][1][w]; }
+      const int nslot = ntu * (a.M / BMC);
+      double* o = a.out_slots + ((size_t)b * nslot + rt * (a.M / BMC) + mt) * 2;
+      o[0] = S; o[1] = SS;
+    }
+  } else if constexpr (EP == EP_BIAS_ATT) {
+    float csum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = trow(r);
+      const float v = fmaf(acc[r], ws, bias);
+      a.Y[((size_t)b * Tp + t) * a.ldy + m] = v;
+      if (t < T) csum += v;                       // partial mean over frames (per channel)
+      float x = v;                                // partial mean over channels (per frame)
+      x += __shfl_xor(x, 16); x += __shfl_xor(x, 8); x += __shfl_xor(x, 4);
+      x += __shfl_xor(x, 2); x += __shfl_xor(x, 1);
+      if (col == 0) epi[0][wc][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = x;
+    }
+    csum += __shfl_xor(csum, 32);
+    if (half == 0) epi[1][wr][wc * 32 + col] = csum;
+    __syncthreads();
+    if (tid < 64) {
+      a.colsum[((size_t)b * (a.M / BMC) + mt) * Tp + t0 + tid] = epi[0][0][tid] + epi[0][1][tid];
+    } else if (tid < 128) {
+      const int i = tid - 64;
+      a.rowsum[((size_t)b * ntu + rt) * a.M + m0 + i] = epi[1][0][i] + epi[1][1][i];
+    }
+  } else {  // EP_BIAS_OUT
+    float* tr = reinterpret_cast<float*>(&sm);  // [64 m][65] transpose staging for the freq-major copy
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = trow(r);
+      const float v = fmaf(acc[r], ws, bias);
+      if (m < a.Mreal) a.Y[((size_t)b * Tp + t) * a.ldy + m] = v;
+      if (a.Yside) tr[(wc * 32 + col) * 65 + (t - t0)] = v;
+    }
+    if (a.Yside) {
+      __syncthreads();
+      for (int i = tid; i < BMC * BT; i += 256) {
+        const int ml = i / BT, tl = i % BT;
+        const int mm = m0 + ml, t = t0 + tl;
+        if (mm < a.Mreal && t < T) a.Yside[((size_t)b * a.Mreal + mm) * T + t] = tr[ml * 65 + tl];
+      }
+    }
+  }
+}
+
+template <int PREC, int EP>
+static hipError_t dispatch_ld(const GemmArgs& a, dim3 grid, hipStream_t s) {
+  const dim3 block(256);
+  const int lm = a.ld.mode;
+  if (a.ld.head) {
+    if constexpr (EP == EP_BIAS_OUT) {
+      switch (lm) {
+        case LD_RECURSIVE: hipLaunchKernelGGL((k_gemm<PREC, LD_RECURSIVE, 1, EP>), grid, block, 0, s, a); break;
+        case LD_RESIDUAL: hipLaunchKernelGGL((k_gemm<PREC, LD_RESIDUAL, 1, EP>), grid, block, 0, s, a); break;
+        case LD_ADD: hipLaunchKernelGGL((k_gemm<PREC, LD_ADD, 1, EP>), grid, block, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  if constexpr (EP == EP_PRELU_STATS) {
+    switch (lm) {
+      case LD_GN: hipLaunchKernelGGL((k_gemm<PREC, LD_GN, 0, EP>), grid, block, 0, s, a); break;
+      case LD_RECURSIVE: hipLaunchKernelGGL((k_gemm<PREC, LD_RECURSIVE, 0, EP>), grid, block, 0, s, a); break;
+      case LD_RESIDUAL: hipLaunchKernelGGL((k_gemm<PREC, LD_RESIDUAL, 0, EP>), grid, block, 0, s, a); break;
+      case LD_ADD: hipLaunchKernelGGL((k_gemm<PREC, LD_ADD, 0, EP>), grid, block, 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if constexpr (EP == EP_BIAS_ATT) {
+    if (lm != LD_DW) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_gemm<PREC, LD_DW, 0, EP>), grid, block, 0, s, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int PREC>
+static hipError_t dispatch_ep(const GemmArgs& a, int ep, dim3 grid, hipStream_t s) {
+  switch (ep) {
+    case EP_PRELU_STATS: return dispatch_ld<PREC, EP_PRELU_STATS>(a, grid, s);
+    case EP_BIAS_ATT: return dispatch_ld<PREC, EP_BIAS_ATT>(a, grid, s);
+    case EP_BIAS_OUT: return dispatch_ld<PREC, EP_BIAS_OUT>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s) {
+  if (a.M % BMC || a.K % BK || a.Tp % BT || a.K > KMAX) return hipErrorInvalidValue;
+  if (a.ld.mode == LD_DW && (a.K != HID || a.ld.dil < 1 || a.ld.dil > 4)) return hipErrorInvalidValue;
+  const dim3 grid(a.B * (a.Tp / BT), a.M / BMC);
+  if (a.prec == PREC_F16X3) return dispatch_ep<PREC_F16X3>(a, ep, grid, s);
+  return dispatch_ep<PREC_F32>(a, ep, grid, s);
+}
+
+}  // namespace sepvad

@@ -1,13 +1,14 @@
 // Internal declarations shared by the kernel translation units and the C-ABI layer.
 // Layout conventions (see DESIGN.md "Data layout in HBM"):
-//   * every per-utterance activation is channel-major [B][rows][Tp], Tp = roundup(T, 64); columns
-//     t >= T are padding whose contents are never reduced over nor used as conv context;
-//   * complex spectra are interleaved float2 [B][257][Tp];
-//   * GroupNorm statistics travel as deterministic per-workgroup partial slots
-//     [B][nslots][2] (sum, sumsq) in double, or per-channel moments [B][C][5] — never atomics,
-//     so results are bitwise reproducible run to run and shard to shard.
+//   * TCN activations are channel-last per utterance: [B][Tp][C], Tp = roundup(T, 64); rows
+//     t >= T are padding that is never reduced over nor used as conv context (zero-padding is
+//     applied explicitly), so a GEMM tile of 64 rows never straddles two utterances;
+//   * spectra are frame-major: X [B][Tp][257] complex (float2), specdb [B][Tp][SPEC_LD];
+//   * GroupNorm statistics travel as deterministic per-workgroup partial records in double
+//     (never float atomics), so results are bitwise reproducible run to run and shard to shard.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include <cstdint>
 
 namespace sepvad {
@@ -18,141 +19,156 @@ constexpr int NBIN = 257;   // n_fftBins/2+1
 constexpr int CH = 256;     // BN_dim == TCN input channels (non-DC bins)
 constexpr int HID = 512;    // H_dim (depthwise multiplier 2)
 constexpr int TILE = 64;    // GEMM tile edge; Tp is a multiple of TILE
-constexpr int MOUT_PAD = 576;  // 2*257 = 514 output-head rows padded to a multiple of 64
+constexpr int MOUT = 2 * NBIN;  // 514 output-head rows (2 speakers x 257 bins)
+constexpr int MOUT_PAD = 576;   // padded to a multiple of 64 (also the row stride of `masks`)
+constexpr int SPEC_LD = 260;    // row stride of the frame-major dB spectrum
+constexpr int STAT_ROWS = 8;    // rows (frames) per workgroup of the stats kernels
+constexpr int NMOM = 11;        // moment record of k_att_stats (see device_common.h)
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
-// Loader transform applied to the GEMM B operand as it is staged (normalize-on-load).
+enum Precision { PREC_F32 = 0, PREC_F16X3 = 1 };
+
+// Residual-stream transform applied to the GEMM A operand as it is staged (normalize-on-load).
 enum LoadMode {
   LD_PLAIN = 0,      // x
-  LD_GN = 1,         // GroupNorm(1,K)(x)                       (stats from slots)
-  LD_RECURSIVE = 2,  // GN_b(o + GN_a(u))   model/model.py:347-348 (stats from moments)
-  LD_RESIDUAL = 3,   // o + GN_c(u)         model/model.py:349-350 (stats of u from slots)
-  LD_ADD = 4         // o + u               model/model.py:351-352
+  LD_GN = 1,         // GroupNorm(1,K)(x)                              (stats: slots)
+  LD_RECURSIVE = 2,  // GN_b(o + GN_a(o + r'))   model/model.py:347-348 (stats: moment records)
+  LD_RESIDUAL = 3,   // o + GN_c(r')             model/model.py:349-350 (stats of r': records)
+  LD_ADD = 4,        // o + r'                   model/model.py:351-352
+  LD_DW = 5          // GN2(PReLU(dconv(GN1(a))))  model/model.py:132-136 (res_out operand)
 };
-// GEMM epilogue.
+// r' = r * (a_f[c] * a_t[t])  (TF_Attention, model/model.py:206-207), or r when tf_attention is off.
+
 enum EpiMode {
   EP_PRELU_STATS = 0,  // + bias, PReLU, store, GN partial stats       (DepthConv1d.conv1d)
-  EP_BIAS_ATT = 1,     // + bias, store, column/row partial sums        (DepthConv1d.res_out -> TF_Attention)
-  EP_BIAS_OUT = 2      // + bias, store rows < Mreal (+ optional de-padded copy)  (TCN.output.2)
+  EP_BIAS_ATT = 1,     // + bias, store, channel/time partial sums      (DepthConv1d.res_out -> TF_Attention)
+  EP_BIAS_OUT = 2      // + bias, store columns < Mreal, optional freq-major copy  (TCN.output.2)
 };
 
-// Parameters of a GN-style loader transform (shared by the GEMM loader and head_prep).
 struct LoadSpec {
   int mode;
-  const float* X;        // [B][K][Tp]  o (or x)
-  const float* X2;       // [B][K][Tp]  u (RECURSIVE/RESIDUAL/ADD)
-  const float* g1; const float* be1; float eps1;  // GN (LD_GN), GN_a (RECURSIVE), GN_c (RESIDUAL)
+  const float* X;        // [B][Tp][K]  o (or x, or a for LD_DW)
+  const float* X2;       // [B][Tp][K]  r (res_out output) for RECURSIVE/RESIDUAL/ADD
+  const float* at;       // [B][Tp] time gate  (nullable => 1)
+  const float* af;       // [B][K]  freq gate  (nullable => 1)
+  const float* g1; const float* be1; float eps1;  // GN (LD_GN), GN_a (RECURSIVE), GN_c (RESIDUAL), GN2 (LD_DW)
   const float* g2; const float* be2; float eps2;  // GN_b (RECURSIVE)
-  const double* slots; int nslots;                // [B][nslots][2]
-  const double* moments;                          // [B][K][5]: S_o, S_oo, S_u, S_uu, S_ou
+  const double* slots; int nslots; int sstride;   // partial records [B][nslots][sstride]
+  // head: x' = GN_out(PReLU(transform(x)))  (model/model.py:322-325)
+  int head;
+  float alpha_h; const float* gh; const float* beh; float epsh;
+  const double* slots_h; int nslots_h;
+  // LD_DW: a -> GN1 -> dconv (k=3, dilation dil, groups=C/2... 2 outputs per input channel) -> PReLU
+  const float* wd; const float* bd; float alpha_d; int dil;
+  const float* gd1; const float* bed1; const double* slots_d1; int nslots_d1;
 };
 
 struct GemmArgs {
-  int B, T, Tp, M, Mreal, K;
-  const float* WT;     // [K][M] (M padded to a multiple of 64)
-  const float* bias;   // [M]
+  int B, T, Tp, M, Mreal, K, ldy;
+  int prec;
+  const float* W32;                        // [M][K] fp32 (PREC_F32)
+  const __half* Whi; const __half* Wlo;    // [M][K] fp16 split of (w * 2^-e_m)  (PREC_F16X3)
+  const float* wscale;                     // [M] 2^e_m (F16X3)
+  const float* bias;                       // [M]
   float prelu;
   LoadSpec ld;
-  float* Xmat;         // nullable: transformed B operand written once (by m-tile 0)
-  float* Y;            // [B][Mreal][Tp]
-  float* Yside;        // nullable [B][Mreal][T]
-  double* out_slots;   // EP_PRELU_STATS [B][(M/64)*(Tp/64)][2]
-  float* colsum;       // EP_BIAS_ATT [B][M/64][Tp]
-  float* rowsum;       // EP_BIAS_ATT [B][Tp/64][M]
+  float* Xmat;          // nullable: transformed A operand x' written once (by m-tile 0), [B][Tp][K]
+  float* Y;             // [B][Tp][ldy]
+  float* Yside;         // nullable [B][Mreal][T] (freq-major copy: self.masks_b)
+  double* out_slots;    // EP_PRELU_STATS: [B][(Tp/64)*(M/64)][2]
+  float* colsum;        // EP_BIAS_ATT: [B][M/64][Tp]   partial sums over channels
+  float* rowsum;        // EP_BIAS_ATT: [B][Tp/64][M]   partial sums over frames
 };
 
-struct DwArgs {
+struct DwStatsArgs {     // statistics of d = PReLU(dconv(GN1(a))) for GN2 (reg2)
   int B, T, Tp, dil;
-  const float* A;                 // [B][CH][Tp] PReLU(conv1d) output (pre-GN1)
-  const double* slots; int nslots;
-  const float* g1; const float* be1;  // reg1
-  const float* wd; const float* bd;   // [HID][3], [HID]
-  float alpha;                        // nonlinearity2
-  float* D;                           // [B][HID][Tp]
-  double* out_slots;                  // [B][CH/16][2]
+  const float* A;        // [B][Tp][CH]
+  const double* slots; int nslots;  // GN1 partials (from the conv1d GEMM epilogue)
+  const float* g1; const float* be1;
+  const float* wd; const float* bd; float alpha;
+  double* out_slots;     // [B][Tp/STAT_ROWS][2]
 };
 
-struct AttArgs {
+struct AttStatsArgs {    // TF-attention gates + the moment records of the residual update
   int B, T, Tp, mtiles, ntiles, tf_att, ln_mode;
-  const float* R;        // [B][CH][Tp] res_out output
-  const float* O;        // [B][CH][Tp] block input o
+  const float* R;        // [B][Tp][CH]
+  const float* O;        // [B][Tp][CH]
   const float* colsum;   // [B][mtiles][Tp]
   const float* rowsum;   // [B][ntiles][CH]
-  const float* attp;     // 16 floats: t1w[3] t1b t2w[3] t2b f1w[3] f1b f2w[3] f2b ; prelu_t, prelu_f at [16],[17]
-  float* U;              // [B][CH][Tp]
-  double* moments;       // [B][CH][5]   (recursive)
-  double* out_slots;     // [B][CH/16][2] (residual: sum/sumsq of r')
+  const float* attp;     // t1w[3] t1b t2w[3] t2b f1w[3] f1b f2w[3] f2b ; [16] prelu_t, [17] prelu_f
+  const float* ga; const float* bea;  // GN_a (recursive) affine: weights of the moment record
+  float* at;             // [B][Tp]
+  float* af;             // [B][CH]
+  double* out_mom;       // [B][Tp/STAT_ROWS][NMOM]
 };
 
-struct HeadPrepArgs {
+struct HeadStatsArgs {   // statistics of PReLU(o_final) for TCN.output.1
   int B, T, Tp;
-  LoadSpec ld;           // final block's o_new transform
-  float alpha;           // TCN.output.0 PReLU
-  float* P;              // [B][CH][Tp]
-  double* out_slots;     // [B][CH/16][2]
+  LoadSpec ld;
+  double* out_slots;     // [B][Tp/STAT_ROWS][2]
 };
 
 struct GateArgs {
   int B, T, Tp, activity;
-  const float* specdb;   // [B][NBIN][Tp] 10log10(clamp(|X|^2,1e-10)), DC row = -100
+  const float* specdb;   // [B][Tp][SPEC_LD]
   const float* w;        // activity_input.weight [9] ; bias at w[9]; prelu at w[10]
-  float* S0;             // [B][CH][Tp] gated rows 1..256
-  float* spec_side;      // nullable [B][NBIN][T]
-  double* out_slots;     // [B][gate_tiles][2]
+  float* S0;             // [B][Tp][CH] gated bins 1..256
+  float* spec_side;      // nullable [B][NBIN][T] (self.spectrum)
+  double* out_slots;     // [B][Tp/16][2]
 };
-
 constexpr int GATE_ROWS = 16;
-__host__ __device__ constexpr int gate_tiles() { return (NBIN + GATE_ROWS - 1) / GATE_ROWS; }
 
 struct StftArgs {
   int B, N, T, Tp;
   const float* x;        // [B][N]
   const float* window;   // [512]
   const float2* tw;      // [512] e^{-2 pi i m / 512}
-  float2* X;             // [B][NBIN][Tp]  (workspace) or nullable
+  float2* X;             // nullable [B][Tp][NBIN]
   float2* Xout;          // nullable [B][NBIN][T] (debug entry)
-  float* specdb;         // nullable [B][NBIN][Tp]
-  float* spec_out;       // nullable [B][NBIN][T]
+  float* specdb;         // nullable [B][Tp][SPEC_LD]
+  float* spec_out;       // nullable [B][NBIN][T] (debug entry)
 };
 
-struct VadArgs {
-  int B, T, Tp, masked_speakers, noisy_phase;
-  const float* masks;    // [B][2*NBIN][Tp] pre-sigmoid
-  const float2* X;       // [B][NBIN][Tp]
+constexpr int VAD_ROWS = 16;
+struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4) partial stats
+  int B, T, Tp, masked_speakers;
+  const float* masks;    // [B][Tp][MOUT_PAD] pre-sigmoid
+  const float2* X;       // [B][Tp][NBIN]
   const float* w1;       // [4][257][5]
   const float* b1;       // [4]
-  float alpha;           // relu_1
-  const float* g;        // BN_1 weight [4]
-  const float* be;       // BN_1 bias [4]
-  const float* w2;       // [4][3]
-  float b2;
-  int kw_enabled, filt, ret_smooth;
-  float thr;
-  float* vad_out;        // [B][2][T]
-  float* gain;           // [B][2][Tp]
+  float alpha;
+  float* vy;             // [B][2][4][Tp]
+  double* out_slots;     // [B][2][Tp/VAD_ROWS][2]
 };
 
 struct IstftArgs {
-  int BS, S, N, T, Tp, noisy_phase, est_mode;  // est_mode 1: apply mask to X (forward); 0: est given
-  const float2* X;       // [B][NBIN][Tp]  (est_mode 1)
-  const float* masks;    // [B][S*NBIN][Tp] pre-sigmoid (est_mode 1)
-  const float* gain;     // nullable [B][S][Tp]
+  int BS, S, N, T, Tp, est_mode;  // est_mode 1: forward (mask X, VAD); 0: est given (debug entry)
+  const float2* X;       // [B][Tp][NBIN]
+  const float* masks;    // [B][Tp][MOUT_PAD] pre-sigmoid
   const float2* est_in;  // [BS][NBIN][T] (est_mode 0)
   const float* window;   // [512]
   const float2* tw;      // [512]
+  // VAD tail (model/model.py:160-179,444-457); has_vad = 0 -> no VAD, gain 1
+  int has_vad, kw_enabled, filt, ret_smooth;
+  float thr;
+  const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output
+  const double* vslots; int nvslots;
+  const float* vg; const float* vbe;  // BN_1 affine [4]
+  const float* w2; float b2;          // output_layer_vad [4][3], bias
+  float* vad_out;        // [B][S][T]
   float2* est_out;       // nullable [BS][NBIN][T]
   float* mask_out;       // nullable [BS][NBIN][T]
   float* y;              // [BS][N]
 };
 
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
-hipError_t launch_dw(const DwArgs& a, hipStream_t s);
-hipError_t launch_att(const AttArgs& a, hipStream_t s);
-hipError_t launch_head_prep(const HeadPrepArgs& a, hipStream_t s);
+hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);
+hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s);
+hipError_t launch_head_stats(const HeadStatsArgs& a, hipStream_t s);
 hipError_t launch_gate(const GateArgs& a, hipStream_t s);
 hipError_t launch_stft(const StftArgs& a, hipStream_t s);
-hipError_t launch_vad(const VadArgs& a, hipStream_t s);
+hipError_t launch_vad1(const Vad1Args& a, hipStream_t s);
 hipError_t launch_istft(const IstftArgs& a, hipStream_t s);
 
 }  // namespace sepvad

@@ -1,12 +1,14 @@
-// TCN elementwise/reduction kernels (HBM/L2-bound; no MFMA):
-//   k_gate      activity gate: Conv2d(1,1,3x3,pad 1) + PReLU, spectrum *= gate (model/model.py:414-419)
-//               and the TCN.LN partial statistics of rows 1..256 (model/model.py:333,421)
-//   k_dw        GN1 on load -> depthwise dilated conv 256->512 (k=3, groups=256) -> PReLU,
-//               GN2 partial statistics (model/model.py:110-113,132-136)
-//   k_att       TF_Attention gates from the res_out epilogue's partial means, rank-1 scaling,
-//               then u = o + r' (recursive LN) with per-channel moments, or r' with stats
-//               (residual LN) (model/model.py:182-208,345-352)
-//   k_head_prep final o, PReLU of TCN.output.0 and GN statistics of TCN.output.1 (model/model.py:322-325)
+// TCN reduction kernels (HBM/L2-bound, no MFMA), channel-last [B][Tp][C]:
+//   k_gate        activity gate: Conv2d(1,1,3x3,pad 1) on the dB spectrum + PReLU, spectrum *= gate
+//                 (model/model.py:414-419); writes the TCN input (bins 1..256) and the TCN.LN
+//                 partial statistics (model/model.py:333,421)
+//   k_dw_stats    statistics of d = PReLU(dconv(GN1(a))) for reg2 (model/model.py:132-136); d itself is
+//                 recomputed inside the res_out GEMM's operand loader and never stored
+//   k_att_stats   TF_Attention gates a_t, a_f (model/model.py:197-205) from the res_out epilogue's partial
+//                 means, and the moment records that give the recursive/residual LN statistics
+//                 (model/model.py:345-350) without materializing u or v
+//   k_head_stats  statistics of PReLU(o_final) for TCN.output.1 (model/model.py:322-325)
+// Workgroup = (utterance, STAT_ROWS frames), thread = channel: every row access is a coalesced 1 KB read.
 #include "device_common.h"
 
 namespace sepvad {
@@ -14,19 +16,18 @@ namespace sepvad {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
   constexpr int R = GATE_ROWS;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int W = a.Tp + 2;
-  float* tile = smem;                     // [R+2][Tp+2]
+  __shared__ float S[R + 2][NBIN + 2];   // dB spectrum rows t0-1..t0+R, bins -1..257 (zero padded)
+  __shared__ float G[R][NBIN + 1];       // gated spectrum
   __shared__ double red[16];
-  const int b = blockIdx.x, r0 = blockIdx.y * R;
+  const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int tid = threadIdx.x;
-  const float* sp = a.specdb + (size_t)b * NBIN * a.Tp;
-  for (int i = tid; i < (R + 2) * W; i += blockDim.x) {
-    const int rr = i / W, tt = i % W;
-    const int f = r0 - 1 + rr, t = tt - 1;
+  const int T = a.T;
+  for (int i = tid; i < (R + 2) * (NBIN + 2); i += 256) {
+    const int rr = i / (NBIN + 2), ff = i % (NBIN + 2);
+    const int t = t0 - 1 + rr, f = ff - 1;
     float v = 0.f;
-    if (f >= 0 && f < NBIN && t >= 0 && t < a.T) v = sp[(size_t)f * a.Tp + t];
-    tile[i] = v;
+    if (t >= 0 && t < T && f >= 0 && f < NBIN) v = a.specdb[((size_t)b * a.Tp + t) * SPEC_LD + f];
+    S[rr][ff] = v;
   }
   __syncthreads();
   float w[9];
@@ -34,258 +35,227 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
   for (int i = 0; i < 9; ++i) w[i] = a.w[i];
   const float bias = a.w[9], alpha = a.w[10];
   double s = 0.0, ss = 0.0;
-  for (int i = tid; i < R * a.Tp; i += blockDim.x) {
-    const int rr = i / a.Tp, t = i % a.Tp;
-    const int f = r0 + rr;
-    if (f >= NBIN) continue;
-    const float x = tile[(rr + 1) * W + t + 1];
+  for (int i = tid; i < R * NBIN; i += 256) {
+    const int ti = i / NBIN, f = i % NBIN;
+    const int t = t0 + ti;
+    const float x = S[ti + 1][f + 1];
     float y = x;
     if (a.activity) {
+      // out[f][t] = b + sum_{i,j} w[i][j] s[f+i-1][t+j-1]  (weight [1,1,3(F),3(T)])
       float g = bias;
 #pragma unroll
       for (int di = 0; di < 3; ++di)
 #pragma unroll
-        for (int dj = 0; dj < 3; ++dj) g = fmaf(w[di * 3 + dj], tile[(rr + di) * W + t + dj], g);
+        for (int dj = 0; dj < 3; ++dj) g = fmaf(w[di * 3 + dj], S[ti + dj][f + di], g);
       y = x * prelu_f(g, alpha);
     }
-    if (f >= 1) a.S0[((size_t)b * CH + f - 1) * a.Tp + t] = y;
-    if (t < a.T) {
-      if (a.spec_side) a.spec_side[((size_t)b * NBIN + f) * a.T + t] = y;
-      if (f >= 1) { s += y; ss += (double)y * y; }
-    }
+    G[ti][f] = y;
+    if (f >= 1) a.S0[((size_t)b * a.Tp + t) * CH + f - 1] = y;
+    if (t < T && f >= 1) { s += y; ss += (double)y * y; }
   }
   s = block_sum(s, red);
   ss = block_sum(ss, red);
   if (tid == 0) {
-    double* o = a.out_slots + ((size_t)b * gate_tiles() + blockIdx.y) * 2;
+    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
     o[0] = s; o[1] = ss;
+  }
+  if (a.spec_side) {  // self.spectrum, [B][257][T]: 16 consecutive frames per bin
+    for (int i = tid; i < NBIN * R; i += 256) {
+      const int f = i / R, ti = i % R, t = t0 + ti;
+      if (t < T) a.spec_side[((size_t)b * NBIN + f) * T + t] = G[ti][f];
+    }
   }
 }
 
 hipError_t launch_gate(const GateArgs& a, hipStream_t s) {
-  dim3 grid(a.B, gate_tiles());
-  size_t lds = (size_t)(GATE_ROWS + 2) * (a.Tp + 2) * sizeof(float);
-  hipLaunchKernelGGL(k_gate, grid, dim3(256), lds, s, a);
+  if (a.Tp % GATE_ROWS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gate, dim3(a.B, a.Tp / GATE_ROWS), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-constexpr int DW_CH = 16;   // input channels per workgroup (-> 32 output channels)
-constexpr int DW_HALO = 4;  // max dilation
-
-__global__ __launch_bounds__(256) void k_dw(DwArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int W = a.Tp + 2 * DW_HALO;
-  float* h = smem;  // [DW_CH][W]
+__global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
+  constexpr int R = STAT_ROWS;
+  __shared__ float H[R + 8][CH];   // GN1(a) rows t0-dil .. t0+R+dil (zero outside [0,T))
   __shared__ double red[16];
   __shared__ float bc[4];
-  const int b = blockIdx.x, c0 = blockIdx.y * DW_CH;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
+  const int b = blockIdx.x, t0 = blockIdx.y * R;
+  const int c = threadIdx.x;
+  const int T = a.T, dl = a.dil;
+  if (c == 0) {
     float mu, rs;
-    slots_stats(a.slots + (size_t)b * a.nslots * 2, a.nslots, (double)CH * a.T, 1e-8f, mu, rs);
+    slots_stats(a.slots + (size_t)b * a.nslots * 2, a.nslots, 2, (double)CH * T, 1e-8f, mu, rs);
     bc[0] = mu; bc[1] = rs;
   }
   __syncthreads();
-  const float mu = bc[0], rs = bc[1];
-  for (int i = tid; i < DW_CH * W; i += blockDim.x) {
-    const int c = i / W, tt = i % W, t = tt - DW_HALO;
-    float v = 0.f;
-    if (t >= 0 && t < a.T) {
-      const float s = rs * a.g1[c0 + c];
-      const float sh = a.be1[c0 + c] - s * mu;
-      v = fmaf(a.A[((size_t)b * CH + c0 + c) * a.Tp + t], s, sh);
-    }
-    h[i] = v;
+  const float sc = bc[1] * a.g1[c];
+  const float sh = a.be1[c] - sc * bc[0];
+  for (int rr = 0; rr < R + 2 * dl; ++rr) {
+    const int t = t0 - dl + rr;
+    H[rr][c] = (t >= 0 && t < T) ? fmaf(a.A[((size_t)b * a.Tp + t) * CH + c], sc, sh) : 0.f;
   }
-  __syncthreads();
-  const int d = a.dil;
+  // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2)
   double s = 0.0, ss = 0.0;
-  for (int i = tid; i < 2 * DW_CH * a.Tp; i += blockDim.x) {
-    const int jj = i / a.Tp, t = i % a.Tp;
-    const int j = 2 * c0 + jj, c = jj >> 1;
-    const float* hr = h + c * W + DW_HALO + t;
-    float v = a.bd[j];
-    v = fmaf(a.wd[j * 3 + 0], hr[-d], v);
-    v = fmaf(a.wd[j * 3 + 1], hr[0], v);
-    v = fmaf(a.wd[j * 3 + 2], hr[d], v);
-    v = prelu_f(v, a.alpha);
-    a.D[((size_t)b * HID + j) * a.Tp + t] = v;
-    if (t < a.T) { s += v; ss += (double)v * v; }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int j = 2 * c + q;
+    const float w0 = a.wd[j * 3 + 0], w1 = a.wd[j * 3 + 1], w2 = a.wd[j * 3 + 2], bj = a.bd[j];
+    for (int i = 0; i < R; ++i) {
+      if (t0 + i >= T) break;
+      float v = bj;
+      v = fmaf(w0, H[i][c], v);
+      v = fmaf(w1, H[i + dl][c], v);
+      v = fmaf(w2, H[i + 2 * dl][c], v);
+      v = prelu_f(v, a.alpha);
+      s += v; ss += (double)v * v;
+    }
   }
   s = block_sum(s, red);
   ss = block_sum(ss, red);
-  if (tid == 0) {
-    double* o = a.out_slots + ((size_t)b * (CH / DW_CH) + blockIdx.y) * 2;
+  if (c == 0) {
+    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
     o[0] = s; o[1] = ss;
   }
 }
 
-hipError_t launch_dw(const DwArgs& a, hipStream_t s) {
-  if (a.dil < 1 || a.dil > DW_HALO) return hipErrorInvalidValue;
-  dim3 grid(a.B, CH / DW_CH);
-  size_t lds = (size_t)DW_CH * (a.Tp + 2 * DW_HALO) * sizeof(float);
-  hipLaunchKernelGGL(k_dw, grid, dim3(256), lds, s, a);
+hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s) {
+  if (a.dil < 1 || a.dil > 4 || a.Tp % STAT_ROWS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dw_stats, dim3(a.B, a.Tp / STAT_ROWS), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-constexpr int ATT_CH = 16;
-
-__global__ __launch_bounds__(256) void k_att(AttArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  // LDS: mc[Tp+8], y1[Tp+8], at[Tp], mf[ATT_CH+12], yf1[ATT_CH+12], af[ATT_CH]
-  const int Wt = a.Tp + 8;
-  float* mc = smem;
-  float* y1 = mc + Wt;
-  float* at = y1 + Wt;
-  float* mf = at + a.Tp;
-  float* yf1 = mf + (ATT_CH + 12);
-  float* af = yf1 + (ATT_CH + 12);
+__global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
+  constexpr int R = STAT_ROWS;
+  __shared__ float mT[CH + 8], yf[CH + 8], afs[CH];
+  __shared__ float mC[R + 8], yt[R + 8], ats[R];
   __shared__ double red[16];
-  const int b = blockIdx.x, c0 = blockIdx.y * ATT_CH;
-  const int tid = threadIdx.x;
+  const int b = blockIdx.x, t0 = blockIdx.y * R;
+  const int c = threadIdx.x;
   const int T = a.T;
-
   if (a.tf_att) {
     const float* p = a.attp;
-    // time gate a_t: mean over channels (AdaptiveAvgPool2d((1,None))), conv d=1 -> conv d=2 -> PReLU -> sigmoid
-    for (int i = tid; i < Wt; i += blockDim.x) {
-      const int t = i - 4;
+    // a_f: mean over frames (AdaptiveAvgPool2d((None,1))) -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid
+    {
+      float sacc = 0.f;
+      for (int q = 0; q < a.ntiles; ++q) sacc += a.rowsum[((size_t)b * a.ntiles + q) * CH + c];
+      mT[c + 4] = sacc / (float)T;
+      if (c < 4) { mT[c] = 0.f; mT[CH + 4 + c] = 0.f; yf[c] = 0.f; yf[CH + 4 + c] = 0.f; }
+    }
+    // a_t rows t0-4 .. t0+R+4: mean over channels (AdaptiveAvgPool2d((1,None)))
+    if (c < R + 8) {
+      const int t = t0 - 4 + c;
       float v = 0.f;
       if (t >= 0 && t < T) {
         float sacc = 0.f;
         for (int q = 0; q < a.mtiles; ++q) sacc += a.colsum[((size_t)b * a.mtiles + q) * a.Tp + t];
         v = sacc / (float)CH;
       }
-      mc[i] = v;
+      mC[c] = v;
     }
     __syncthreads();
-    for (int i = tid; i < Wt; i += blockDim.x) {
-      const int t = i - 4;
+    yf[c + 4] = p[11] + p[8] * mT[c + 3] + p[9] * mT[c + 4] + p[10] * mT[c + 5];
+    if (c < R + 8) {
+      const int t = t0 - 4 + c;
       float v = 0.f;
-      if (t >= 0 && t < T) v = p[3] + p[0] * mc[i - 1] + p[1] * mc[i] + p[2] * mc[i + 1];
-      y1[i] = v;
+      if (t >= 0 && t < T && c >= 1 && c < R + 7) v = p[3] + p[0] * mC[c - 1] + p[1] * mC[c] + p[2] * mC[c + 1];
+      yt[c] = v;
     }
     __syncthreads();
-    for (int t = tid; t < a.Tp; t += blockDim.x) {
-      const int i = t + 4;
-      const float v = p[7] + p[4] * y1[i - 2] + p[5] * y1[i] + p[6] * y1[i + 2];
-      at[t] = sigmoid_f(prelu_f(v, p[16]));
+    {
+      const float v = p[15] + p[12] * yf[c + 2] + p[13] * yf[c + 4] + p[14] * yf[c + 6];
+      afs[c] = sigmoid_f(prelu_f(v, p[17]));
     }
-    // frequency gate a_f for channels c0..c0+15 (needs means of c0-3 .. c0+18)
-    for (int i = tid; i < ATT_CH + 12; i += blockDim.x) {
-      const int c = c0 - 6 + i;
-      float v = 0.f;
-      if (c >= 0 && c < CH) {
-        float sacc = 0.f;
-        for (int q = 0; q < a.ntiles; ++q) sacc += a.rowsum[((size_t)b * a.ntiles + q) * CH + c];
-        v = sacc / (float)T;
-      }
-      mf[i] = v;
+    if (c < R) {
+      const int k = c + 4;
+      const float v = p[7] + p[4] * yt[k - 2] + p[5] * yt[k] + p[6] * yt[k + 2];
+      ats[c] = sigmoid_f(prelu_f(v, p[16]));
     }
     __syncthreads();
-    for (int i = tid; i < ATT_CH + 12; i += blockDim.x) {
-      const int c = c0 - 6 + i;
-      float v = 0.f;
-      if (c >= 0 && c < CH && i >= 1 && i < ATT_CH + 11)
-        v = p[11] + p[8] * mf[i - 1] + p[9] * mf[i] + p[10] * mf[i + 1];
-      yf1[i] = v;
-    }
-    __syncthreads();
-    for (int i = tid; i < ATT_CH; i += blockDim.x) {
-      const int k = i + 6;
-      const float v = p[15] + p[12] * yf1[k - 2] + p[13] * yf1[k] + p[14] * yf1[k + 2];
-      af[i] = sigmoid_f(prelu_f(v, p[17]));
-    }
-    __syncthreads();
-  }
-
-  // main sweep: 16 channels x Tp, 16 threads per channel
-  const int cg = tid >> 4, l16 = tid & 15;
-  const int c = c0 + cg;
-  const size_t rowoff = ((size_t)b * CH + c) * a.Tp;
-  double So = 0, Soo = 0, Su = 0, Suu = 0, Sou = 0;
-  const float afc = a.tf_att ? af[cg] : 1.f;
-  for (int t = l16; t < a.Tp; t += 16) {
-    const float r = a.R[rowoff + t];
-    float rp = r;
-    if (a.tf_att) rp = r * (afc * at[t]);  // attention_w = a_f @ a_t, then input * attention_w
-    float u = rp;
-    if (a.ln_mode == LD_RECURSIVE) {
-      const float o = a.O[rowoff + t];
-      u = o + rp;
-      if (t < T) { So += o; Soo += (double)o * o; Su += u; Suu += (double)u * u; Sou += (double)o * u; }
-    } else if (t < T) {
-      Su += u; Suu += (double)u * u;
-    }
-    a.U[rowoff + t] = u;
-  }
-  // reduce within the 16-lane channel group
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    So += __shfl_xor(So, o); Soo += __shfl_xor(Soo, o); Su += __shfl_xor(Su, o);
-    Suu += __shfl_xor(Suu, o); Sou += __shfl_xor(Sou, o);
-  }
-  if (a.ln_mode == LD_RECURSIVE) {
-    if (l16 == 0) {
-      double* m = a.moments + ((size_t)b * CH + c) * 5;
-      m[0] = So; m[1] = Soo; m[2] = Su; m[3] = Suu; m[4] = Sou;
-    }
+    if (blockIdx.y == 0) a.af[(size_t)b * CH + c] = afs[c];
+    if (c < R) a.at[(size_t)b * a.Tp + t0 + c] = ats[c];
   } else {
-    // per-workgroup partial (sum, sumsq) of r' in channel order
-    __shared__ double cs[2][ATT_CH];
-    if (l16 == 0) { cs[0][cg] = Su; cs[1][cg] = Suu; }
+    afs[c] = 1.f;
+    if (c < R) ats[c] = 1.f;
     __syncthreads();
-    if (tid == 0) {
-      double s = 0, ss = 0;
-      for (int i = 0; i < ATT_CH; ++i) { s += cs[0][i]; ss += cs[1][i]; }
-      double* o = a.out_slots + ((size_t)b * (CH / ATT_CH) + blockIdx.y) * 2;
-      o[0] = s; o[1] = ss;
+  }
+  // moment record over this workgroup's frames (t < T)
+  const bool rec = a.ln_mode == LD_RECURSIVE;
+  const double g = rec ? (double)a.ga[c] : 0.0, be = rec ? (double)a.bea[c] : 0.0;
+  double m[NMOM];
+#pragma unroll
+  for (int j = 0; j < NMOM; ++j) m[j] = 0.0;
+  const float afc = afs[c];
+  for (int i = 0; i < R; ++i) {
+    const int t = t0 + i;
+    if (t >= T) break;
+    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
+    const float r = a.R[off];
+    const float rp = a.tf_att ? r * (afc * ats[i]) : r;
+    if (rec) {
+      const float of = a.O[off];
+      const float uf = of + rp;
+      const double o = of, u = uf;
+      m[0] += o; m[1] += o * o; m[2] += u; m[3] += u * u; m[4] += be * o; m[5] += g * u;
+      m[6] += g * o * u; m[7] += g * o; m[8] += g * be * u; m[9] += g * g * u * u; m[10] += g * g * u;
+    } else {
+      const double u = rp;
+      m[2] += u; m[3] += u * u;
     }
   }
-  (void)red;
+  double* o = a.out_mom + ((size_t)b * (a.Tp / R) + blockIdx.y) * NMOM;
+#pragma unroll
+  for (int j = 0; j < NMOM; ++j) {
+    if (!rec && j != 2 && j != 3) { if (c == 0) o[j] = 0.0; continue; }
+    const double v = block_sum(m[j], red);
+    if (c == 0) o[j] = v;
+  }
 }
 
-hipError_t launch_att(const AttArgs& a, hipStream_t s) {
-  dim3 grid(a.B, CH / ATT_CH);
-  size_t lds = (size_t)(2 * (a.Tp + 8) + a.Tp + 3 * (ATT_CH + 12)) * sizeof(float);
-  hipLaunchKernelGGL(k_att, grid, dim3(256), lds, s, a);
+hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s) {
+  if (a.Tp % STAT_ROWS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_att_stats, dim3(a.B, a.Tp / STAT_ROWS), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-constexpr int HP_CH = 16;
-
-__global__ __launch_bounds__(256) void k_head_prep(HeadPrepArgs a) {
+__global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
+  constexpr int R = STAT_ROWS;
   __shared__ float cf[4][CH];
   __shared__ double red[16];
   __shared__ float bc[4];
-  const int b = blockIdx.x, c0 = blockIdx.y * HP_CH;
-  const int tid = threadIdx.x;
-  loader_coefs(a.ld, b, CH, a.T, cf[0], cf[1], cf[2], cf[3], red, bc);
+  const int b = blockIdx.x, t0 = blockIdx.y * R;
+  const int c = threadIdx.x;
+  const LoadSpec& ld = a.ld;
+  resid_coefs(ld, b, CH, a.T, cf[0], cf[1], cf[2], cf[3], red, bc);
+  const float afc = ld.af ? ld.af[(size_t)b * CH + c] : 1.f;
   double s = 0.0, ss = 0.0;
-  for (int i = tid; i < HP_CH * a.Tp; i += blockDim.x) {
-    const int c = c0 + i / a.Tp, t = i % a.Tp;
-    const size_t off = ((size_t)b * CH + c) * a.Tp + t;
-    const float x = a.ld.X[off];
-    const float u = (a.ld.mode == LD_PLAIN || a.ld.mode == LD_GN) ? 0.f : a.ld.X2[off];
-    const float o = loader_apply(a.ld.mode, x, u, c, cf[0], cf[1], cf[2], cf[3]);
-    const float p = prelu_f(o, a.alpha);
-    a.P[off] = p;
-    if (t < a.T) { s += p; ss += (double)p * p; }
+  for (int i = 0; i < R; ++i) {
+    const int t = t0 + i;
+    if (t >= a.T) break;
+    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
+    const float o = ld.X[off], r = ld.X2[off];
+    const float g = afc * (ld.at ? ld.at[(size_t)b * a.Tp + t] : 1.f);
+    float x;
+    switch (ld.mode) {
+      case LD_RECURSIVE: x = resid_apply<LD_RECURSIVE>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
+      case LD_RESIDUAL: x = resid_apply<LD_RESIDUAL>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
+      default: x = resid_apply<LD_ADD>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
+    }
+    const float p = prelu_f(x, ld.alpha_h);
+    s += p; ss += (double)p * p;
   }
   s = block_sum(s, red);
   ss = block_sum(ss, red);
-  if (tid == 0) {
-    double* o = a.out_slots + ((size_t)b * (CH / HP_CH) + blockIdx.y) * 2;
+  if (c == 0) {
+    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
     o[0] = s; o[1] = ss;
   }
 }
 
-hipError_t launch_head_prep(const HeadPrepArgs& a, hipStream_t s) {
-  dim3 grid(a.B, CH / HP_CH);
-  hipLaunchKernelGGL(k_head_prep, grid, dim3(256), 0, s, a);
+hipError_t launch_head_stats(const HeadStatsArgs& a, hipStream_t s) {
+  if (a.Tp % STAT_ROWS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_head_stats, dim3(a.B, a.Tp / STAT_ROWS), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -17,6 +17,8 @@ CPU fallback — a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -151,6 +153,9 @@ class SeparationModel(nn.Module):
             self.prelu = _PReLU()
         self._handles = {}
         self.register_load_state_dict_post_hook(lambda module, keys: module._invalidate_native())
+        # GEMM arithmetic of the native path: "f16x3" (fp32-equivalent split on fp16 MFMA, default)
+        # or "fp32" (fp32 MFMA); both meet the fp32 parity gates. SEPVAD_PRECISION overrides.
+        self.native_precision = os.environ.get("SEPVAD_PRECISION", "f16x3")
 
     # -- native handle -------------------------------------------------------------------------
     # The handle (folded, packed device weights) is rebuilt lazily after load_state_dict(),
@@ -174,8 +179,10 @@ class SeparationModel(nn.Module):
         h = self._handles.get(device)
         if h is None:
             sd = {k: v.detach() for k, v in self.state_dict().items()}
-            h = _native.Handle(self._cfg, sd, device)
+            h = _native.Handle(self._cfg, sd, device, self.native_precision)
             self._handles[device] = h
+        elif h.precision != self.native_precision:
+            h.set_precision(self.native_precision)
         return h
 
     # -- forward (model/model.py:402-461) --------------------------------------------------------

@@ -15,10 +15,11 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsepvad.so")
 
 SEPVAD_LN_PLAIN, SEPVAD_LN_RECURSIVE, SEPVAD_LN_RESIDUAL = 0, 1, 2
-SEPVAD_PREC_FP32 = 0
+SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3 = 0, 1
+PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3}
 
 EXPORTED_SYMBOLS = (
-    "sepvad_create", "sepvad_reserve", "sepvad_forward", "sepvad_stft", "sepvad_istft",
+    "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_stft", "sepvad_istft",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
 
@@ -59,6 +60,8 @@ def load_library(path: str = LIB_PATH):
                                   ctypes.POINTER(ctypes.c_int64), i32, i32]
     lib.sepvad_reserve.restype = i32
     lib.sepvad_reserve.argtypes = [P, i32, i32]
+    lib.sepvad_set_precision.restype = i32
+    lib.sepvad_set_precision.argtypes = [P, i32]
     lib.sepvad_forward.restype = i32
     lib.sepvad_forward.argtypes = [P, P, i32, i32, ctypes.POINTER(SepVadOutputs), ctypes.POINTER(SepVadInferKw), P]
     lib.sepvad_stft.restype = i32
@@ -85,7 +88,7 @@ def _check(rc, what):
         raise RuntimeError(f"{what} failed (status {rc}): {msg}")
 
 
-def make_config(cfg: dict) -> SepVadConfig:
+def make_config(cfg: dict, precision: str = "f16x3") -> SepVadConfig:
     c = SepVadConfig()
     c.n_fft, c.bn_dim, c.h_dim = cfg["n_fftBins"], cfg["BN_dim"], cfg["H_dim"]
     c.layer, c.stack, c.num_spk = cfg["layer"], cfg["stack"], cfg["num_spk"]
@@ -96,7 +99,7 @@ def make_config(cfg: dict) -> SepVadConfig:
     c.final_vad_masked_speakers = int(bool(cfg["final_vad_masked_speakers"]))
     c.noisy_phase = int(bool(cfg["noisy_phase"]))
     c.activity_input = int(bool(cfg["activity_input_bool"]))
-    c.precision = SEPVAD_PREC_FP32
+    c.precision = PRECISIONS[precision]
     return c
 
 
@@ -122,7 +125,7 @@ def _ptr(t):
 class Handle:
     """Owns one ``sepvad_handle`` (device weights + workspace) for one device."""
 
-    def __init__(self, cfg: dict, state_dict: dict, device):
+    def __init__(self, cfg: dict, state_dict: dict, device, precision: str = "f16x3"):
         lib = load_library()
         device = torch.device(device)
         if device.type != "cuda":
@@ -136,7 +139,8 @@ class Handle:
         ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, t in host])
         names = (ctypes.c_char_p * n)(*[k.encode() for k, _ in host])
         numels = (ctypes.c_int64 * n)(*[t.numel() for _, t in host])
-        self._c = make_config(cfg)
+        self._c = make_config(cfg, precision)
+        self.precision = precision
         h = lib.sepvad_create(ctypes.byref(self._c), ptrs, names, numels, n, self.index)
         if not h:
             raise RuntimeError("sepvad_create failed: " + lib.sepvad_last_error().decode(errors="replace"))
@@ -155,6 +159,10 @@ class Handle:
 
     def reserve(self, B: int, N: int):
         _check(self._lib.sepvad_reserve(self._h, B, N), "sepvad_reserve")
+
+    def set_precision(self, precision: str):
+        _check(self._lib.sepvad_set_precision(self._h, PRECISIONS[precision]), "sepvad_set_precision")
+        self.precision = precision
 
     def set_timing(self, on: bool):
         _check(self._lib.sepvad_set_timing(self._h, int(on)), "sepvad_set_timing")

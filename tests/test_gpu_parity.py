@@ -22,9 +22,12 @@ def _model(cname, state_dicts):
     return net.eval().to(DEV)
 
 
-@pytest.fixture(scope="module")
-def models(state_dicts):
-    return {c: _model(c, state_dicts) for c in CONFIGS}
+@pytest.fixture(scope="module", params=["f16x3", "fp32"])
+def models(request, state_dicts):
+    out = {c: _model(c, state_dicts) for c in CONFIGS}
+    for m in out.values():
+        m.native_precision = request.param
+    return out
 
 
 def test_native_library_is_loaded():
@@ -104,8 +107,8 @@ def test_stft_kernel_vs_torch(models):
         assert X.shape == Xr.shape
         assert (X - Xr).abs().max().item() <= 2e-5 * Xr.abs().max().item() + 1e-5
         sr = 10 * torch.log10(torch.clamp(Xr.abs() ** 2, min=1e-10))
-        ok = Xr.abs() > 1e-3
-        assert (spec - sr)[ok].abs().max().item() <= 1e-3
+        ok = Xr.abs() > 1e-2  # dB of tiny bins amplifies fp32 rounding (d dB = 8.7 |dX|/|X|)
+        assert (spec - sr)[ok].abs().max().item() <= 2e-3
 
 
 def test_istft_kernel_vs_torch(models):
