@@ -33,6 +33,7 @@ METRIC = "utterances/sec/GPU (4s@8kHz, 2spk+VAD); SI-SDR within 0.01 dB of ref"
 B_PER_GPU = 64
 N_SAMPLES = 32000
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix (= vector) peak, dense
+F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: BF16/F16 dense MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -79,6 +80,8 @@ def main():
     ap.add_argument("--samples", type=int, default=N_SAMPLES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
+                    help="GEMM arithmetic (both meet the fp32 parity gates; see DESIGN.md)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,6 +107,7 @@ def main():
     sd = synth.make_state_dict(cfg, 1234)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     net = net.eval().to(dev)
+    net.native_precision = args.precision
     B, N = args.batch, args.samples
     T = 1 + N // 256
     # this rank's shard of utterances: global utterance ids [rank*B, (rank+1)*B)
@@ -154,6 +158,14 @@ def main():
         value = total_utt / el
         res_avg_s = res_ms / n_res / 1e3
         achieved = res_out_flops(B, T) / res_avg_s / 1e12
+        # peak of the arithmetic actually issued: fp16x3 issues 3 fp16 MFMA products per fp32 product
+        if args.precision == "f16x3":
+            peak, kern = F16_MFMA_PEAK_TFLOPS / 3.0, ("k_gemm<F16X3,LD_DW,EP_BIAS_ATT> (DepthConv1d.res_out 512->256 "
+                                                     "with the depthwise conv fused in the operand loader; fp16x3 "
+                                                     "split on v_mfma_f32_32x32x16_f16: peak = 2.5 PF/s / 3)")
+        else:
+            peak, kern = FP32_MFMA_PEAK_TFLOPS, ("k_gemm<F32,LD_DW,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, "
+                                                 "v_mfma_f32_32x32x2_f32)")
         fwd_timed = n_gemm / (2 * 24 + 1)  # 49 GEMM launches per forward
         all_gemm_tflops = gemm_flops_per_utt(T) * B * fwd_timed / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
         traffic = None
@@ -175,6 +187,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "gemm_arithmetic": args.precision,
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
                     "recipe weights (pretrained .pth absent from the reference)",
             "config": {
@@ -187,11 +200,11 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "k_pw_gemm<LD_GN,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, fp32 MFMA 32x32x2)",
+                "kernel": kern,
                 "achieved": round(achieved, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "peak": round(peak, 1),
                 "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "frac": round(achieved / peak, 4),
                 "traffic": traffic,
                 "flops_per_launch": res_out_flops(B, T),
                 "avg_launch_us": round(res_avg_s * 1e6, 2),

@@ -48,6 +48,7 @@ struct BlockOff {
   size_t b1, g1, be1, wd, bd, b2, g2, be2, attp, lna_g, lna_b, lnb_g, lnb_b;
   float a1, a2;
   int dil;
+  double wsum[5];  // {Σγa, Σβa, Σβa², Σγa·βa, Σγa²} of ln_first (closed-form recursive-LN stats)
 };
 
 struct Workspace {
@@ -56,7 +57,8 @@ struct Workspace {
   size_t bytes = 0;
   float2* X; float* specdb; float* S0; float* O[2]; float* A; float* R;
   float* masks; float* colsum; float* rowsum; float* at; float* af; float* vy; float* vad;
-  double* sl_gate; double* sl_g1; double* sl_dw; double* mom; double* sl_hs; double* sl_vad;
+  // partial records of the statistics producers (deterministic per-workgroup sums)
+  double* rec_gate; double* rec_g1; double* rec_dw; double* rec_mom; double* rec_hs; double* rec_vad;
 };
 
 }  // namespace
@@ -180,9 +182,9 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   const size_t oM = take(bt * MOUT_PAD * 4);
   const size_t oCs = take(bt * (CH / TILE) * 4), oRs = take((size_t)Bm * (Tm / TILE) * CH * 4);
   const size_t oAt = take(bt * 4), oAf = take((size_t)Bm * CH * 4), oVy = take(bt * 2 * 4 * 4), oV = take(bt * 2 * 4);
-  const size_t oSg = take(bt / GATE_ROWS * 16 + 16), oS1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
-  const size_t oSd = take(bt / STAT_ROWS * 16 + 16), oMo = take(bt / STAT_ROWS * NMOM * 8 + 16);
-  const size_t oSh = take(bt / STAT_ROWS * 16 + 16), oSv = take(bt * 2 / VAD_ROWS * 16 + 16);
+  const size_t oRg = take(bt / GATE_ROWS * 16 + 16), oR1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
+  const size_t oRd = take(bt / STAT_ROWS * 16 + 16), oRm = take(bt / STAT_ROWS * NMOM * 8 + 16);
+  const size_t oRh = take(bt / STAT_ROWS * 16 + 16), oRv = take(bt * 2 / VAD_ROWS * 16 + 16);
   char* base = nullptr;
   HIPCHK(hipMalloc(&base, off));
   HIPCHK(hipMemset(base, 0, off));
@@ -193,8 +195,8 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   w.R = (float*)(base + oR); w.masks = (float*)(base + oM);
   w.colsum = (float*)(base + oCs); w.rowsum = (float*)(base + oRs); w.at = (float*)(base + oAt);
   w.af = (float*)(base + oAf); w.vy = (float*)(base + oVy); w.vad = (float*)(base + oV);
-  w.sl_gate = (double*)(base + oSg); w.sl_g1 = (double*)(base + oS1); w.sl_dw = (double*)(base + oSd);
-  w.mom = (double*)(base + oMo); w.sl_hs = (double*)(base + oSh); w.sl_vad = (double*)(base + oSv);
+  w.rec_gate = (double*)(base + oRg); w.rec_g1 = (double*)(base + oR1); w.rec_dw = (double*)(base + oRd);
+  w.rec_mom = (double*)(base + oRm); w.rec_hs = (double*)(base + oRh); w.rec_vad = (double*)(base + oRv);
   return SEPVAD_OK;
 }
 
@@ -229,6 +231,12 @@ void set_weights(const sepvad_model* h, GemmArgs& g, const PackedW& w) {
 }
 
 // The residual-stream transform that turns (o_i, r_i) of block i into the next block input.
+GnSrc gn_src(const double* rec, int nrec, int rstride, int roff, const float* g, const float* be, float eps) {
+  GnSrc s;
+  s.rec = rec; s.nrec = nrec; s.rstride = rstride; s.roff = roff; s.g = g; s.be = be; s.eps = eps;
+  return s;
+}
+
 LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float* R, int Tp) {
   LoadSpec ld{};
   ld.X = O; ld.X2 = R;
@@ -236,13 +244,12 @@ LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float
   const BlockOff& bo = h->blk[i];
   if (h->cfg.ln_mode == SEPVAD_LN_RECURSIVE) {
     ld.mode = LD_RECURSIVE;
-    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
+    ld.gn = gn_src(h->ws.rec_mom, Tp / STAT_ROWS, NMOM, 0, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
     ld.g2 = h->P(bo.lnb_g); ld.be2 = h->P(bo.lnb_b); ld.eps2 = 1e-5f;
-    ld.slots = h->ws.mom; ld.nslots = Tp / STAT_ROWS; ld.sstride = NMOM;
+    for (int j = 0; j < 5; ++j) ld.wsum[j] = bo.wsum[j];
   } else if (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL) {
-    ld.mode = LD_RESIDUAL;
-    ld.g1 = h->P(bo.lna_g); ld.be1 = h->P(bo.lna_b); ld.eps1 = 1e-5f;
-    ld.slots = h->ws.mom + 2; ld.nslots = Tp / STAT_ROWS; ld.sstride = NMOM;  // (Σr', Σr'²) at 2, 3
+    ld.mode = LD_RESIDUAL;  // (Σr', Σr'²) at offsets 2, 3 of the moment record
+    ld.gn = gn_src(h->ws.rec_mom, Tp / STAT_ROWS, NMOM, 2, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
   } else {
     ld.mode = LD_ADD;
   }
@@ -366,6 +373,11 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       BAIL();
       bo.lna_g = pk.add(fa, CH); bo.lna_b = pk.add(fb, CH);
       bo.lnb_g = pk.add(sa, CH); bo.lnb_b = pk.add(sb, CH);
+      for (int j = 0; j < 5; ++j) bo.wsum[j] = 0.0;
+      for (int k = 0; k < CH; ++k) {
+        const double g = fa[k], e = fb[k];
+        bo.wsum[0] += g; bo.wsum[1] += e; bo.wsum[2] += e * e; bo.wsum[3] += g * e; bo.wsum[4] += g * g;
+      }
     } else if (c.ln_mode == SEPVAD_LN_RESIDUAL) {
       const float* fa = get("TCN.ln_modules." + std::to_string(i) + ".weight", CH);
       const float* fb = get("TCN.ln_modules." + std::to_string(i) + ".bias", CH);
@@ -504,12 +516,11 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     GateArgs ga{};
     ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
     ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = w.S0; ga.spec_side = out->spectrum;
-    ga.out_slots = w.sl_gate;
+    ga.out_rec = w.rec_gate;
     HIPCHK(launch_gate(ga, s));
   }
   // 3. TCN blocks
   int cur = 0;  // w.O[cur] holds the current block input o once the conv1d GEMM materialized it
-  const int nsl_g1 = ntu * (CH / TILE);
   for (int i = 0; i < h->nblk; ++i) {
     const BlockOff& bo = h->blk[i];
     const int nxt = (i == 0) ? 0 : (cur ^ 1);
@@ -518,14 +529,14 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     set_weights(h, g, bo.w1);
     g.bias = h->P(bo.b1); g.prelu = bo.a1;
     if (i == 0) {
-      g.ld.mode = LD_GN; g.ld.X = w.S0;
-      g.ld.g1 = h->P(h->ln_g); g.ld.be1 = h->P(h->ln_b); g.ld.eps1 = 1e-8f;
-      g.ld.slots = w.sl_gate; g.ld.nslots = Tp / GATE_ROWS; g.ld.sstride = 2;
+      g.ld.mode = LD_GN; g.ld.X = w.S0;   // TCN.LN (model/model.py:333)
+      g.ld.gn = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
     } else {
       g.ld = residual_spec(h, i - 1, w.O[cur], w.R, Tp);
     }
     g.Xmat = w.O[nxt];
-    g.Y = w.A; g.out_slots = w.sl_g1;
+    g.Y = w.A;
+    g.out_rec = w.rec_g1;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
     if (ev_record(h, s)) return SEPVAD_E_HIP;
@@ -534,20 +545,18 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
 
     DwStatsArgs d{};
     d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
-    d.slots = w.sl_g1; d.nslots = nsl_g1;
-    d.g1 = h->P(bo.g1); d.be1 = h->P(bo.be1); d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
-    d.out_slots = w.sl_dw;
+    const GnSrc gn1 = gn_src(w.rec_g1, ntu * (CH / TILE), 2, 0, h->P(bo.g1), h->P(bo.be1), 1e-8f);
+    d.gd1 = gn1; d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
+    d.out_rec = w.rec_dw;
     HIPCHK(launch_dw_stats(d, s));
 
     GemmArgs g2{};
     g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
     set_weights(h, g2, bo.w2);
     g2.bias = h->P(bo.b2);
-    g2.ld.mode = LD_DW; g2.ld.X = w.A;
-    g2.ld.g1 = h->P(bo.g2); g2.ld.be1 = h->P(bo.be2); g2.ld.eps1 = 1e-8f;
-    g2.ld.slots = w.sl_dw; g2.ld.nslots = Tp / STAT_ROWS; g2.ld.sstride = 2;
+    g2.ld.mode = LD_DW; g2.ld.X = w.A; g2.ld.gd1 = gn1;
+    g2.ld.gn = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, h->P(bo.g2), h->P(bo.be2), 1e-8f);
     g2.ld.wd = h->P(bo.wd); g2.ld.bd = h->P(bo.bd); g2.ld.alpha_d = bo.a2; g2.ld.dil = bo.dil;
-    g2.ld.gd1 = h->P(bo.g1); g2.ld.bed1 = h->P(bo.be1); g2.ld.slots_d1 = w.sl_g1; g2.ld.nslots_d1 = nsl_g1;
     g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
@@ -560,7 +569,7 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     at.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     at.R = w.R; at.O = w.O[cur]; at.colsum = w.colsum; at.rowsum = w.rowsum; at.attp = h->P(bo.attp);
     if (c.ln_mode == SEPVAD_LN_RECURSIVE) { at.ga = h->P(bo.lna_g); at.bea = h->P(bo.lna_b); }
-    at.at = w.at; at.af = w.af; at.out_mom = w.mom;
+    at.at = w.at; at.af = w.af; at.out_rec = w.rec_mom;
     HIPCHK(launch_att_stats(at, s));
   }
   // 4. output head: PReLU -> GN(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
@@ -569,15 +578,15 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     hs.B = B; hs.T = T; hs.Tp = Tp;
     hs.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
     hs.ld.alpha_h = h->out_a;
-    hs.out_slots = w.sl_hs;
+    hs.out_rec = w.rec_hs;
     HIPCHK(launch_head_stats(hs, s));
     GemmArgs g{};
     g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
     set_weights(h, g, h->wout);
     g.bias = h->P(h->bo);
     g.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
-    g.ld.head = 1; g.ld.alpha_h = h->out_a; g.ld.gh = h->P(h->out_g); g.ld.beh = h->P(h->out_b);
-    g.ld.epsh = 1e-5f; g.ld.slots_h = w.sl_hs; g.ld.nslots_h = Tp / STAT_ROWS;
+    g.ld.head = 1; g.ld.alpha_h = h->out_a;
+    g.ld.gh = gn_src(w.rec_hs, Tp / STAT_ROWS, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
     g.Y = w.masks; g.Yside = out->masks_b;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
@@ -592,7 +601,7 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     v.B = B; v.T = T; v.Tp = Tp; v.masked_speakers = c.final_vad_masked_speakers;
     v.masks = w.masks; v.X = w.X;
     v.w1 = h->P(h->v_w1); v.b1 = h->P(h->v_b1); v.alpha = h->v_a;
-    v.vy = w.vy; v.out_slots = w.sl_vad;
+    v.vy = w.vy; v.out_rec = w.rec_vad;
     HIPCHK(launch_vad1(v, s));
   }
   // 6. VAD tail + est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-460)
@@ -607,8 +616,8 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
       is.filt = kw_on && (kw->filter_signals_by_smo_vad || kw->filter_signals_by_unsmo_vad);
       is.ret_smooth = kw_on && kw->return_smoothed_vad;
       is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
-      is.vy = w.vy; is.vslots = w.sl_vad; is.nvslots = Tp / VAD_ROWS;
-      is.vg = h->P(h->v_g); is.vbe = h->P(h->v_b); is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
+      is.vy = w.vy; is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
+      is.vgn = gn_src(w.rec_vad, Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
       is.vad_out = out->vad ? out->vad : w.vad;
     }
     is.est_out = (float2*)out->est; is.mask_out = out->mask; is.y = out->sep;

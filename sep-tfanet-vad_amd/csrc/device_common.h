@@ -34,6 +34,25 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
+// Reduce NV per-thread float values over the block (deterministic: fixed shuffle tree, waves
+// summed in order, in double) and store them to `out[0..NV)` from thread 0. One barrier.
+// `lds` holds >= NV * 16 floats.
+template <int NV>
+__device__ __forceinline__ void block_reduce_store(float (&v)[NV], float* lds, double* out) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float s = wave_sum(v[j]);
+    if (l == 0) lds[j * 16 + w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+    for (int i = 0; i < nw; ++i) s += lds[threadIdx.x * 16 + i];
+    out[threadIdx.x] = s;
+  }
+}
+
 // (mean, rstd) from partial (sum, sumsq) records summed in record order; torch: biased variance,
 // rstd = 1/sqrt(max(var,0)+eps).
 __device__ __forceinline__ void slots_stats(const double* p, int n, int stride, double count, float eps,
@@ -45,83 +64,6 @@ __device__ __forceinline__ void slots_stats(const double* p, int n, int stride, 
   if (var < 0.0) var = 0.0;
   mean = (float)mu;
   rstd = (float)(1.0 / sqrt(var + (double)eps));
-}
-
-// GN affine coefficients for channels [0, K) from slots (thread 0 finalizes, all threads fill).
-__device__ inline void gn_coefs(const double* slots, int nslots, int stride, double count, float eps,
-                                const float* g, const float* be, int K, float* s, float* h, float* bc) {
-  if (threadIdx.x == 0) {
-    float mu, rs;
-    slots_stats(slots, nslots, stride, count, eps, mu, rs);
-    bc[0] = mu; bc[1] = rs;
-  }
-  __syncthreads();
-  const float mu = bc[0], rs = bc[1];
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const float sc = rs * g[k];
-    s[k] = sc;
-    h[k] = be[k] - sc * mu;
-  }
-  __syncthreads();
-}
-
-// Recursive-LN coefficients (model/model.py:347-348) from the moment records of k_att_stats:
-//   u = o + r', v = o + GN_a(u), o_new = GN_b(v);   record (per element, g = gamma_a[c], be = beta_a[c]):
-//   0 Σo  1 Σo²  2 Σu  3 Σu²  4 Σbe·o  5 Σg·u  6 Σg·o·u  7 Σg·o  8 Σg·be·u  9 Σg²·u²  10 Σg²·u
-// Σv and Σv² follow in closed form (v = (o+be) + ra·g·(u-μa)), so v is never materialized.
-// Outputs c0 = sa, c1 = ha (GN_a), c2 = sb, c3 = hb (GN_b). All threads must call (barriers).
-__device__ inline void recursive_coefs(const LoadSpec& ld, int b, int K, int T, float* c0, float* c1,
-                                       float* c2, float* c3, double* red, float* bc) {
-  const int tid = threadIdx.x;
-  double gs = 0, bs = 0, bbs = 0, gbs = 0, ggs = 0;
-  for (int k = tid; k < K; k += blockDim.x) {
-    const double g = ld.g1[k], e = ld.be1[k];
-    gs += g; bs += e; bbs += e * e; gbs += g * e; ggs += g * g;
-  }
-  gs = block_sum(gs, red); bs = block_sum(bs, red); bbs = block_sum(bbs, red);
-  gbs = block_sum(gbs, red); ggs = block_sum(ggs, red);
-  if (tid == 0) {
-    const double* p = ld.slots + (size_t)b * ld.nslots * NMOM;
-    double m[NMOM];
-    for (int j = 0; j < NMOM; ++j) m[j] = 0.0;
-    for (int i = 0; i < ld.nslots; ++i)
-      for (int j = 0; j < NMOM; ++j) m[j] += p[(size_t)i * NMOM + j];
-    const double n = (double)K * T, Tn = (double)T;
-    const double mua = m[2] / n;
-    double vara = m[3] / n - mua * mua;
-    if (vara < 0.0) vara = 0.0;
-    const float rsa = (float)(1.0 / sqrt(vara + (double)ld.eps1));
-    const float mua_f = (float)mua;
-    const double ra = rsa, mu = mua_f;
-    const double sv = m[0] + ra * (m[5] - mu * Tn * gs) + Tn * bs;
-    const double svv = m[1] + 2.0 * m[4] + Tn * bbs + 2.0 * ra * (m[6] - mu * m[7] + m[8] - mu * Tn * gbs) +
-                       ra * ra * (m[9] - 2.0 * mu * m[10] + mu * mu * Tn * ggs);
-    const double mub = sv / n;
-    double varb = svv / n - mub * mub;
-    if (varb < 0.0) varb = 0.0;
-    bc[0] = mua_f; bc[1] = rsa;
-    bc[2] = (float)mub; bc[3] = (float)(1.0 / sqrt(varb + (double)ld.eps2));
-  }
-  __syncthreads();
-  const float mua = bc[0], rsa = bc[1], mub = bc[2], rsb = bc[3];
-  for (int k = tid; k < K; k += blockDim.x) {
-    const float sa = rsa * ld.g1[k];
-    c0[k] = sa; c1[k] = ld.be1[k] - sa * mua;
-    const float sb = rsb * ld.g2[k];
-    c2[k] = sb; c3[k] = ld.be2[k] - sb * mub;
-  }
-  __syncthreads();
-}
-
-// Coefficients of the residual-stream transform for utterance b (modes GN/RECURSIVE/RESIDUAL).
-__device__ inline void resid_coefs(const LoadSpec& ld, int b, int K, int T, float* c0, float* c1, float* c2,
-                                   float* c3, double* red, float* bc) {
-  if (ld.mode == LD_GN || ld.mode == LD_RESIDUAL) {
-    gn_coefs(ld.slots + (size_t)b * ld.nslots * ld.sstride, ld.nslots, ld.sstride, (double)K * T, ld.eps1,
-             ld.g1, ld.be1, K, c0, c1, bc);
-  } else if (ld.mode == LD_RECURSIVE) {
-    recursive_coefs(ld, b, K, T, c0, c1, c2, c3, red, bc);
-  }
 }
 
 // x' for one element: o = X value, r = X2 value, g = a_f[k] * a_t[t] (1 when attention is off).
@@ -140,6 +82,79 @@ __device__ __forceinline__ float resid_apply(float o, float r, float g, int k, c
     return o + r * g;
   } else {
     return o;
+  }
+}
+
+
+// ---- consumer-side statistics: partial records -> GroupNorm affine vectors in LDS --------------
+// Records are loaded by all threads in parallel into LDS and summed in record order (fixed =>
+// deterministic, identical in every consumer workgroup). All threads must call (barriers).
+
+// Sum nrec records (stride rs, values at [off, off+nv)) into out[0..nv) (LDS). Thread (g, j) sums
+// value j over records g, g+G, ... in order, then thread j sums the G partials in order.
+// tmp: >= blockDim doubles of LDS.
+__device__ inline void sum_records(const double* rec, int nrec, int rs, int off, int nv, double* tmp, double* out) {
+  const int G = blockDim.x / nv;
+  const int t = threadIdx.x;
+  if (t < G * nv) {
+    const int g = t / nv, j = t % nv;
+    double s = 0.0;
+    for (int r = g; r < nrec; r += G) s += rec[(size_t)r * rs + off + j];
+    tmp[t] = s;
+  }
+  __syncthreads();
+  if (t < nv) {
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += tmp[g * nv + t];
+    out[t] = s;
+  }
+  __syncthreads();
+}
+
+// GroupNorm(1,K) affine (scale s[k], shift h[k]) of utterance b from its (sum, sumsq) records.
+__device__ inline void gn_from_records(const GnSrc& src, int b, int K, int T, float* s, float* h, double* tmp,
+                                       double* acc) {
+  sum_records(src.rec + (size_t)b * src.nrec * src.rstride, src.nrec, src.rstride, src.roff, 2, tmp, acc);
+  const double cnt = (double)K * T;
+  const double mu = acc[0] / cnt;
+  double var = acc[1] / cnt - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float muf = (float)mu, rs = (float)(1.0 / sqrt(var + (double)src.eps));
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float sc = rs * src.g[k];
+    s[k] = sc;
+    h[k] = src.be[k] - sc * muf;
+  }
+}
+
+// Recursive-LN affine (GN_a: sa, ha; GN_b: sb, hb) of utterance b from the moment records
+//   0 Σo  1 Σo²  2 Σu  3 Σu²  4 Σbe·o  5 Σg·u  6 Σg·o·u  7 Σg·o  8 Σg·be·u  9 Σg²·u²  10 Σg²·u
+// (u = o + r', g = gamma_a[c], be = beta_a[c]); v = (o+be) + ra·g·(u-μa) gives Σv, Σv² in closed
+// form, so neither u nor v is materialized. wsum = {Σg, Σbe, Σbe², Σg·be, Σg²} over channels (host).
+__device__ inline void recursive_from_records(const LoadSpec& ld, int b, int K, int T, float* c0, float* c1,
+                                              float* c2, float* c3, double* tmp, double* acc) {
+  sum_records(ld.gn.rec + (size_t)b * ld.gn.nrec * NMOM, ld.gn.nrec, NMOM, 0, NMOM, tmp, acc);
+  const double* m = acc;
+  const double cnt = (double)K * T, Tn = (double)T;
+  const double mua = m[2] / cnt;
+  double vara = m[3] / cnt - mua * mua;
+  if (vara < 0.0) vara = 0.0;
+  const float rsa = (float)(1.0 / sqrt(vara + (double)ld.gn.eps));
+  const float mua_f = (float)mua;
+  const double ra = rsa, mu = mua_f;
+  const double gs = ld.wsum[0], bs = ld.wsum[1], bbs = ld.wsum[2], gbs = ld.wsum[3], ggs = ld.wsum[4];
+  const double sv = m[0] + ra * (m[5] - mu * Tn * gs) + Tn * bs;
+  const double svv = m[1] + 2.0 * m[4] + Tn * bbs + 2.0 * ra * (m[6] - mu * m[7] + m[8] - mu * Tn * gbs) +
+                     ra * ra * (m[9] - 2.0 * mu * m[10] + mu * mu * Tn * ggs);
+  const double mub = sv / cnt;
+  double varb = svv / cnt - mub * mub;
+  if (varb < 0.0) varb = 0.0;
+  const float mub_f = (float)mub, rsb = (float)(1.0 / sqrt(varb + (double)ld.eps2));
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float sa = rsa * ld.gn.g[k];
+    c0[k] = sa; c1[k] = ld.gn.be[k] - sa * mua_f;
+    const float sb = rsb * ld.g2[k];
+    c2[k] = sb; c3[k] = ld.be2[k] - sb * mub_f;
   }
 }
 

@@ -60,8 +60,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   __shared__ float atr[BT];
   __shared__ float wdl[LM == LD_DW ? HID * 4 : 1];  // dconv taps (3) + bias per output channel
   __shared__ float Hs[LM == LD_DW ? DWROWS : 1][LM == LD_DW ? 17 : 1];
-  __shared__ double red[16];
-  __shared__ float bc[4];
+  __shared__ double dtmp[256];
+  __shared__ double dacc[NMOM];
   __shared__ float epi[2][2][64];
 
   const int tid = threadIdx.x;
@@ -73,33 +73,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   const int mt = blockIdx.y, m0 = mt * BMC;
   const int K = a.K, T = a.T, Tp = a.Tp;
   const LoadSpec& ld = a.ld;
-
-  // ---------------- prologue: per-utterance coefficients in LDS ----------------
-  if constexpr (LM == LD_GN || LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
-    resid_coefs(ld, b, K, T, cf[0], cf[1], cf[2], cf[3], red, bc);
-  }
-  if constexpr (LM == LD_DW) {
-    // GN1 over a (CH channels, stats from the conv1d epilogue), GN2 over d (HID channels)
-    gn_coefs(ld.slots_d1 + (size_t)b * ld.nslots_d1 * 2, ld.nslots_d1, 2, (double)CH * T, 1e-8f, ld.gd1,
-             ld.bed1, CH, cf[2], cf[3], bc);
-    gn_coefs(ld.slots + (size_t)b * ld.nslots * ld.sstride, ld.nslots, ld.sstride, (double)HID * T, ld.eps1,
-             ld.g1, ld.be1, HID, cf[0], cf[1], bc);
-    for (int j = tid; j < HID; j += 256) {
-      wdl[j * 4 + 0] = ld.wd[j * 3 + 0];
-      wdl[j * 4 + 1] = ld.wd[j * 3 + 1];
-      wdl[j * 4 + 2] = ld.wd[j * 3 + 2];
-      wdl[j * 4 + 3] = ld.bd[j];
-    }
-  }
-  if constexpr (HEAD) {
-    gn_coefs(ld.slots_h + (size_t)b * ld.nslots_h * 2, ld.nslots_h, 2, (double)K * T, ld.epsh, ld.gh, ld.beh, K,
-             hco[0], hco[1], bc);
-  }
-  if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
-    for (int k = tid; k < K; k += 256) afk[k] = ld.af ? ld.af[(size_t)b * K + k] : 1.f;
-    if (tid < BT) atr[tid] = ld.at ? ld.at[(size_t)b * Tp + t0 + tid] : 1.f;
-  }
-  __syncthreads();
 
   // ---------------- staging: global -> registers -> (transform) -> LDS ----------------
   float4 ro[2], rr[2];
@@ -249,6 +222,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
 
   const int nk = K / BK;
   gather(0);
+  // ---------------- prologue (overlaps the first chunk's loads): GN affines -> LDS ----------------
+  if constexpr (LM == LD_GN || LM == LD_RESIDUAL) gn_from_records(ld.gn, b, K, T, cf[0], cf[1], dtmp, dacc);
+  if constexpr (LM == LD_RECURSIVE) recursive_from_records(ld, b, K, T, cf[0], cf[1], cf[2], cf[3], dtmp, dacc);
+  if constexpr (LM == LD_DW) {
+    gn_from_records(ld.gd1, b, CH, T, cf[2], cf[3], dtmp, dacc);  // GN1 (reg1) over a
+    gn_from_records(ld.gn, b, HID, T, cf[0], cf[1], dtmp, dacc);  // GN2 (reg2) over d
+    for (int j = tid; j < HID; j += 256) {
+      wdl[j * 4 + 0] = ld.wd[j * 3 + 0];
+      wdl[j * 4 + 1] = ld.wd[j * 3 + 1];
+      wdl[j * 4 + 2] = ld.wd[j * 3 + 2];
+      wdl[j * 4 + 3] = ld.bd[j];
+    }
+  }
+  if constexpr (HEAD) gn_from_records(ld.gh, b, K, T, hco[0], hco[1], dtmp, dacc);
+  if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
+    for (int k = tid; k < K; k += 256) afk[k] = ld.af ? ld.af[(size_t)b * K + k] : 1.f;
+    if (tid < BT) atr[tid] = ld.at ? ld.at[(size_t)b * Tp + t0 + tid] : 1.f;
+  }
+  __syncthreads();
+
   stage(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -297,11 +290,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
     ss = wave_sum(ss);
     if (lane == 0) { epi[0][0][wave] = s; epi[0][1][wave] = ss; }
     __syncthreads();
+    const int nslot = ntu * (a.M / BMC);
     if (tid == 0) {
       double S = 0.0, SS = 0.0;
       for (int w = 0; w < 4; ++w) { S += epi[0][0][w]; SS += epi[0][1][w]; }
-      const int nslot = ntu * (a.M / BMC);
-      double* o = a.out_slots + ((size_t)b * nslot + rt * (a.M / BMC) + mt) * 2;
+      double* o = a.out_rec + ((size_t)b * nslot + rt * (a.M / BMC) + mt) * 2;
       o[0] = S; o[1] = SS;
     }
   } else if constexpr (EP == EP_BIAS_ATT) {

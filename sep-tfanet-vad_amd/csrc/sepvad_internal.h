@@ -46,22 +46,30 @@ enum EpiMode {
   EP_BIAS_OUT = 2      // + bias, store columns < Mreal, optional freq-major copy  (TCN.output.2)
 };
 
+// GroupNorm statistics source: partial records [B][nrec][rstride] written by a producer kernel
+// ((sum, sumsq) at [roff, roff+1]); every consumer turns them into the affine in its prologue.
+struct GnSrc {
+  const double* rec; int nrec, rstride, roff;
+  const float* g; const float* be; float eps;
+};
+
 struct LoadSpec {
   int mode;
   const float* X;        // [B][Tp][K]  o (or x, or a for LD_DW)
   const float* X2;       // [B][Tp][K]  r (res_out output) for RECURSIVE/RESIDUAL/ADD
   const float* at;       // [B][Tp] time gate  (nullable => 1)
   const float* af;       // [B][K]  freq gate  (nullable => 1)
-  const float* g1; const float* be1; float eps1;  // GN (LD_GN), GN_a (RECURSIVE), GN_c (RESIDUAL), GN2 (LD_DW)
-  const float* g2; const float* be2; float eps2;  // GN_b (RECURSIVE)
-  const double* slots; int nslots; int sstride;   // partial records [B][nslots][sstride]
+  GnSrc gn;              // LD_GN: GN; LD_RESIDUAL: GN_c of r'; LD_RECURSIVE: GN_a (moment records);
+                         // LD_DW: GN2 (reg2) of d
+  const float* g2; const float* be2; float eps2;   // GN_b (recursive)
+  double wsum[5];                                  // recursive: {Σg, Σbe, Σbe², Σg·be, Σg²} of GN_a
   // head: x' = GN_out(PReLU(transform(x)))  (model/model.py:322-325)
   int head;
-  float alpha_h; const float* gh; const float* beh; float epsh;
-  const double* slots_h; int nslots_h;
-  // LD_DW: a -> GN1 -> dconv (k=3, dilation dil, groups=C/2... 2 outputs per input channel) -> PReLU
+  float alpha_h;
+  GnSrc gh;
+  // LD_DW: a -> GN1 -> dconv (k=3, dilation dil, 2 outputs per input channel) -> PReLU
   const float* wd; const float* bd; float alpha_d; int dil;
-  const float* gd1; const float* bed1; const double* slots_d1; int nslots_d1;
+  GnSrc gd1;             // GN1 (reg1) of a
 };
 
 struct GemmArgs {
@@ -76,7 +84,7 @@ struct GemmArgs {
   float* Xmat;          // nullable: transformed A operand x' written once (by m-tile 0), [B][Tp][K]
   float* Y;             // [B][Tp][ldy]
   float* Yside;         // nullable [B][Mreal][T] (freq-major copy: self.masks_b)
-  double* out_slots;    // EP_PRELU_STATS: [B][(Tp/64)*(M/64)][2]
+  double* out_rec;      // EP_PRELU_STATS: [B][(Tp/64)*(M/64)][2] partial (sum, sumsq)
   float* colsum;        // EP_BIAS_ATT: [B][M/64][Tp]   partial sums over channels
   float* rowsum;        // EP_BIAS_ATT: [B][Tp/64][M]   partial sums over frames
 };
@@ -84,10 +92,9 @@ struct GemmArgs {
 struct DwStatsArgs {     // statistics of d = PReLU(dconv(GN1(a))) for GN2 (reg2)
   int B, T, Tp, dil;
   const float* A;        // [B][Tp][CH]
-  const double* slots; int nslots;  // GN1 partials (from the conv1d GEMM epilogue)
-  const float* g1; const float* be1;
+  GnSrc gd1;             // GN1 (reg1) of a
   const float* wd; const float* bd; float alpha;
-  double* out_slots;     // [B][Tp/STAT_ROWS][2]
+  double* out_rec;       // [B][Tp/STAT_ROWS][2]
 };
 
 struct AttStatsArgs {    // TF-attention gates + the moment records of the residual update
@@ -100,13 +107,13 @@ struct AttStatsArgs {    // TF-attention gates + the moment records of the resid
   const float* ga; const float* bea;  // GN_a (recursive) affine: weights of the moment record
   float* at;             // [B][Tp]
   float* af;             // [B][CH]
-  double* out_mom;       // [B][Tp/STAT_ROWS][NMOM]
+  double* out_rec;       // [B][Tp/STAT_ROWS][NMOM]
 };
 
 struct HeadStatsArgs {   // statistics of PReLU(o_final) for TCN.output.1
   int B, T, Tp;
   LoadSpec ld;
-  double* out_slots;     // [B][Tp/STAT_ROWS][2]
+  double* out_rec;       // [B][Tp/STAT_ROWS][2]
 };
 
 struct GateArgs {
@@ -115,7 +122,7 @@ struct GateArgs {
   const float* w;        // activity_input.weight [9] ; bias at w[9]; prelu at w[10]
   float* S0;             // [B][Tp][CH] gated bins 1..256
   float* spec_side;      // nullable [B][NBIN][T] (self.spectrum)
-  double* out_slots;     // [B][Tp/16][2]
+  double* out_rec;       // [B][Tp/GATE_ROWS][2]
 };
 constexpr int GATE_ROWS = 16;
 
@@ -139,7 +146,7 @@ struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4)
   const float* b1;       // [4]
   float alpha;
   float* vy;             // [B][2][4][Tp]
-  double* out_slots;     // [B][2][Tp/VAD_ROWS][2]
+  double* out_rec;       // [B*2][Tp/VAD_ROWS][2]
 };
 
 struct IstftArgs {
@@ -153,8 +160,7 @@ struct IstftArgs {
   int has_vad, kw_enabled, filt, ret_smooth;
   float thr;
   const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output
-  const double* vslots; int nvslots;
-  const float* vg; const float* vbe;  // BN_1 affine [4]
+  GnSrc vgn;             // BN_1 = GroupNorm(1, 4) over [4, T] per (utterance, speaker); rec [B*S][..]
   const float* w2; float b2;          // output_layer_vad [4][3], bias
   float* vad_out;        // [B][S][T]
   float2* est_out;       // nullable [BS][NBIN][T]

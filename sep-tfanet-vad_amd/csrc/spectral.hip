@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   constexpr int R = VAD_ROWS;
   __shared__ float Mt[R + 4][NBIN + 1];   // input rows t0-2 .. t0+R+1
   __shared__ float part[16][R][4];
-  __shared__ double red[16];
+  __shared__ float red[2 * 16];
   const int tid = threadIdx.x;
   const int bs = blockIdx.x, b = bs >> 1, s = bs & 1;
   const int t0 = blockIdx.y * R;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   }
   part[g][i][0] = acc0; part[g][i][1] = acc1; part[g][i][2] = acc2; part[g][i][3] = acc3;
   __syncthreads();
-  double sm = 0.0, ssm = 0.0;
+  float st[2] = {0.f, 0.f};
   if (tid < 4 * R) {
     const int ii = tid >> 2, o = tid & 3;
     const int t = t0 + ii;
@@ -180,14 +180,10 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
     for (int q = 0; q < 16; ++q) y += part[q][ii][o];
     const float v = prelu_f(y + a.b1[o], a.alpha);
     a.vy[(((size_t)b * 2 + s) * 4 + o) * a.Tp + t] = (t < T) ? v : 0.f;
-    if (t < T) { sm = v; ssm = (double)v * v; }
+    if (t < T) { st[0] = v; st[1] = v * v; }
   }
-  sm = block_sum(sm, red);
-  ssm = block_sum(ssm, red);
-  if (tid == 0) {
-    double* o = a.out_slots + (((size_t)b * 2 + s) * (a.Tp / R) + blockIdx.y) * 2;
-    o[0] = sm; o[1] = ssm;
-  }
+  const int nrec = a.Tp / R;
+  block_reduce_store<2>(st, red, a.out_rec + ((size_t)bs * nrec + blockIdx.y) * 2);
 }
 
 hipError_t launch_vad1(const Vad1Args& a, hipStream_t s) {
@@ -209,7 +205,8 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   __shared__ float yn[4][IS_FR + 6];          // GN'd VAD features, frames fbeg-3 .. fbeg+IS_FR+2
   __shared__ float vadv[IS_FR + 4];           // vad at frames fbeg-2 .. fbeg+IS_FR+1
   __shared__ float gain[IS_FR];
-  __shared__ float bc[4];
+  __shared__ float vs[4], vh[4];
+  __shared__ double dtmp[512], dacc[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bs = blockIdx.x, f0 = blockIdx.y * IS_OWN;
   const int T = a.T;
@@ -219,20 +216,13 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
 
   // 0) VAD tail for the frames this block needs
   if (a.est_mode && a.has_vad) {
-    if (tid == 0) {
-      float mu, rs;
-      slots_stats(a.vslots + (size_t)bs * a.nvslots * 2, a.nvslots, 2, 4.0 * T, 1e-8f, mu, rs);
-      bc[0] = mu; bc[1] = rs;
-    }
+    gn_from_records(a.vgn, bs, 4, T, vs, vh, dtmp, dacc);  // BN_1 = GroupNorm(1, 4, eps 1e-8)
     __syncthreads();
     if (tid < 4 * (IS_FR + 6)) {
       const int o = tid / (IS_FR + 6), q = tid % (IS_FR + 6);
       const int f = fbeg - 3 + q;
       float v = 0.f;
-      if (f >= 0 && f < T) {
-        const float sc = bc[1] * a.vg[o];
-        v = fmaf(a.vy[((size_t)bs * 4 + o) * a.Tp + f], sc, a.vbe[o] - sc * bc[0]);
-      }
+      if (f >= 0 && f < T) v = fmaf(a.vy[((size_t)bs * 4 + o) * a.Tp + f], vs[o], vh[o]);
       yn[o][q] = v;
     }
     __syncthreads();

@@ -1,14 +1,16 @@
 // TCN reduction kernels (HBM/L2-bound, no MFMA), channel-last [B][Tp][C]:
 //   k_gate        activity gate: Conv2d(1,1,3x3,pad 1) on the dB spectrum + PReLU, spectrum *= gate
-//                 (model/model.py:414-419); writes the TCN input (bins 1..256) and the TCN.LN
-//                 partial statistics (model/model.py:333,421)
-//   k_dw_stats    statistics of d = PReLU(dconv(GN1(a))) for reg2 (model/model.py:132-136); d itself is
-//                 recomputed inside the res_out GEMM's operand loader and never stored
+//                 (model/model.py:414-419); writes the TCN input (bins 1..256); TCN.LN statistics
+//                 (model/model.py:333,421) records
+//   k_dw_stats    statistics of d = PReLU(dconv(GN1(a))) (model/model.py:132-136) for reg2;
+//                 d itself is recomputed inside the res_out GEMM's operand loader and never stored
 //   k_att_stats   TF_Attention gates a_t, a_f (model/model.py:197-205) from the res_out epilogue's partial
-//                 means, and the moment records that give the recursive/residual LN statistics
-//                 (model/model.py:345-350) without materializing u or v
-//   k_head_stats  statistics of PReLU(o_final) for TCN.output.1 (model/model.py:322-325)
-// Workgroup = (utterance, STAT_ROWS frames), thread = channel: every row access is a coalesced 1 KB read.
+//                 means, and the moment records of the residual update (model/model.py:345-350)
+//                 for the recursive/residual LN, without materializing u or v
+//   k_head_stats  statistics of PReLU(o_final) (model/model.py:322-325) for TCN.output.1
+// Workgroup = (utterance, a few frames), thread = channel: every row access is a coalesced 1 KB read.
+// Each workgroup writes one partial record (deterministic, no atomics); consumers turn the records
+// into GroupNorm affines in their prologues (device_common.h gn_from_records / recursive_from_records).
 #include "device_common.h"
 
 namespace sepvad {
@@ -18,7 +20,7 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
   constexpr int R = GATE_ROWS;
   __shared__ float S[R + 2][NBIN + 2];   // dB spectrum rows t0-1..t0+R, bins -1..257 (zero padded)
   __shared__ float G[R][NBIN + 1];       // gated spectrum
-  __shared__ double red[16];
+  __shared__ float red[2 * 16];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int tid = threadIdx.x;
   const int T = a.T;
@@ -34,7 +36,7 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) w[i] = a.w[i];
   const float bias = a.w[9], alpha = a.w[10];
-  double s = 0.0, ss = 0.0;
+  float st[2] = {0.f, 0.f};
   for (int i = tid; i < R * NBIN; i += 256) {
     const int ti = i / NBIN, f = i % NBIN;
     const int t = t0 + ti;
@@ -51,14 +53,10 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
     }
     G[ti][f] = y;
     if (f >= 1) a.S0[((size_t)b * a.Tp + t) * CH + f - 1] = y;
-    if (t < T && f >= 1) { s += y; ss += (double)y * y; }
+    if (t < T && f >= 1) { st[0] += y; st[1] += y * y; }
   }
-  s = block_sum(s, red);
-  ss = block_sum(ss, red);
-  if (tid == 0) {
-    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
-    o[0] = s; o[1] = ss;
-  }
+  const int nrec = a.Tp / R;
+  block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
   if (a.spec_side) {  // self.spectrum, [B][257][T]: 16 consecutive frames per bin
     for (int i = tid; i < NBIN * R; i += 256) {
       const int f = i / R, ti = i % R, t = t0 + ti;
@@ -77,25 +75,20 @@ hipError_t launch_gate(const GateArgs& a, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
   constexpr int R = STAT_ROWS;
   __shared__ float H[R + 8][CH];   // GN1(a) rows t0-dil .. t0+R+dil (zero outside [0,T))
-  __shared__ double red[16];
-  __shared__ float bc[4];
+  __shared__ float red[2 * 16];
+  __shared__ float s1[CH], h1[CH];
+  __shared__ double dtmp[256], dacc[2];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const int T = a.T, dl = a.dil;
-  if (c == 0) {
-    float mu, rs;
-    slots_stats(a.slots + (size_t)b * a.nslots * 2, a.nslots, 2, (double)CH * T, 1e-8f, mu, rs);
-    bc[0] = mu; bc[1] = rs;
-  }
-  __syncthreads();
-  const float sc = bc[1] * a.g1[c];
-  const float sh = a.be1[c] - sc * bc[0];
+  gn_from_records(a.gd1, b, CH, T, s1, h1, dtmp, dacc);
+  const float sc = s1[c], sh = h1[c];
   for (int rr = 0; rr < R + 2 * dl; ++rr) {
     const int t = t0 - dl + rr;
     H[rr][c] = (t >= 0 && t < T) ? fmaf(a.A[((size_t)b * a.Tp + t) * CH + c], sc, sh) : 0.f;
   }
-  // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2)
-  double s = 0.0, ss = 0.0;
+  // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2); own column only
+  float st[2] = {0.f, 0.f};
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int j = 2 * c + q;
@@ -107,15 +100,11 @@ __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
       v = fmaf(w1, H[i + dl][c], v);
       v = fmaf(w2, H[i + 2 * dl][c], v);
       v = prelu_f(v, a.alpha);
-      s += v; ss += (double)v * v;
+      st[0] += v; st[1] += v * v;
     }
   }
-  s = block_sum(s, red);
-  ss = block_sum(ss, red);
-  if (c == 0) {
-    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
-    o[0] = s; o[1] = ss;
-  }
+  const int nrec = a.Tp / R;
+  block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
 }
 
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s) {
@@ -127,12 +116,13 @@ hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
   constexpr int R = STAT_ROWS;
-  __shared__ float mT[CH + 8], yf[CH + 8], afs[CH];
+  __shared__ float mT[CH + 8], yf[CH + 8];
   __shared__ float mC[R + 8], yt[R + 8], ats[R];
-  __shared__ double red[16];
+  __shared__ float red[NMOM * 16];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const int T = a.T;
+  float afc = 1.f;
   if (a.tf_att) {
     const float* p = a.attp;
     // a_f: mean over frames (AdaptiveAvgPool2d((None,1))) -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid
@@ -164,7 +154,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
     __syncthreads();
     {
       const float v = p[15] + p[12] * yf[c + 2] + p[13] * yf[c + 4] + p[14] * yf[c + 6];
-      afs[c] = sigmoid_f(prelu_f(v, p[17]));
+      afc = sigmoid_f(prelu_f(v, p[17]));
     }
     if (c < R) {
       const int k = c + 4;
@@ -172,20 +162,15 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
       ats[c] = sigmoid_f(prelu_f(v, p[16]));
     }
     __syncthreads();
-    if (blockIdx.y == 0) a.af[(size_t)b * CH + c] = afs[c];
+    if (blockIdx.y == 0) a.af[(size_t)b * CH + c] = afc;
     if (c < R) a.at[(size_t)b * a.Tp + t0 + c] = ats[c];
-  } else {
-    afs[c] = 1.f;
-    if (c < R) ats[c] = 1.f;
-    __syncthreads();
   }
-  // moment record over this workgroup's frames (t < T)
+  // moment record over this workgroup's frames (t < T), see device_common.h finalize_recursive
   const bool rec = a.ln_mode == LD_RECURSIVE;
-  const double g = rec ? (double)a.ga[c] : 0.0, be = rec ? (double)a.bea[c] : 0.0;
-  double m[NMOM];
+  const float g = rec ? a.ga[c] : 0.f, be = rec ? a.bea[c] : 0.f;
+  float m[NMOM];
 #pragma unroll
-  for (int j = 0; j < NMOM; ++j) m[j] = 0.0;
-  const float afc = afs[c];
+  for (int j = 0; j < NMOM; ++j) m[j] = 0.f;
   for (int i = 0; i < R; ++i) {
     const int t = t0 + i;
     if (t >= T) break;
@@ -193,23 +178,16 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
     const float r = a.R[off];
     const float rp = a.tf_att ? r * (afc * ats[i]) : r;
     if (rec) {
-      const float of = a.O[off];
-      const float uf = of + rp;
-      const double o = of, u = uf;
+      const float o = a.O[off];
+      const float u = o + rp;
       m[0] += o; m[1] += o * o; m[2] += u; m[3] += u * u; m[4] += be * o; m[5] += g * u;
       m[6] += g * o * u; m[7] += g * o; m[8] += g * be * u; m[9] += g * g * u * u; m[10] += g * g * u;
     } else {
-      const double u = rp;
-      m[2] += u; m[3] += u * u;
+      m[2] += rp; m[3] += rp * rp;
     }
   }
-  double* o = a.out_mom + ((size_t)b * (a.Tp / R) + blockIdx.y) * NMOM;
-#pragma unroll
-  for (int j = 0; j < NMOM; ++j) {
-    if (!rec && j != 2 && j != 3) { if (c == 0) o[j] = 0.0; continue; }
-    const double v = block_sum(m[j], red);
-    if (c == 0) o[j] = v;
-  }
+  const int nrec = a.Tp / R;
+  block_reduce_store<NMOM>(m, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * NMOM);
 }
 
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s) {
@@ -221,15 +199,17 @@ hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
   constexpr int R = STAT_ROWS;
+  __shared__ float red[2 * 16];
   __shared__ float cf[4][CH];
-  __shared__ double red[16];
-  __shared__ float bc[4];
+  __shared__ double dtmp[256], dacc[NMOM];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const LoadSpec& ld = a.ld;
-  resid_coefs(ld, b, CH, a.T, cf[0], cf[1], cf[2], cf[3], red, bc);
+  if (ld.mode == LD_RECURSIVE) recursive_from_records(ld, b, CH, a.T, cf[0], cf[1], cf[2], cf[3], dtmp, dacc);
+  else if (ld.mode == LD_RESIDUAL) gn_from_records(ld.gn, b, CH, a.T, cf[0], cf[1], dtmp, dacc);
+  __syncthreads();
   const float afc = ld.af ? ld.af[(size_t)b * CH + c] : 1.f;
-  double s = 0.0, ss = 0.0;
+  float st[2] = {0.f, 0.f};
   for (int i = 0; i < R; ++i) {
     const int t = t0 + i;
     if (t >= a.T) break;
@@ -237,20 +217,14 @@ __global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
     const float o = ld.X[off], r = ld.X2[off];
     const float g = afc * (ld.at ? ld.at[(size_t)b * a.Tp + t] : 1.f);
     float x;
-    switch (ld.mode) {
-      case LD_RECURSIVE: x = resid_apply<LD_RECURSIVE>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
-      case LD_RESIDUAL: x = resid_apply<LD_RESIDUAL>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
-      default: x = resid_apply<LD_ADD>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]); break;
-    }
+    if (ld.mode == LD_RECURSIVE) x = resid_apply<LD_RECURSIVE>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]);
+    else if (ld.mode == LD_RESIDUAL) x = resid_apply<LD_RESIDUAL>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]);
+    else x = resid_apply<LD_ADD>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]);
     const float p = prelu_f(x, ld.alpha_h);
-    s += p; ss += (double)p * p;
+    st[0] += p; st[1] += p * p;
   }
-  s = block_sum(s, red);
-  ss = block_sum(ss, red);
-  if (c == 0) {
-    double* o = a.out_slots + ((size_t)b * (a.Tp / R) + blockIdx.y) * 2;
-    o[0] = s; o[1] = ss;
-  }
+  const int nrec = a.Tp / R;
+  block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
 }
 
 hipError_t launch_head_stats(const HeadStatsArgs& a, hipStream_t s) {
