@@ -53,19 +53,6 @@ __device__ __forceinline__ void block_reduce_store(float (&v)[NV], float* lds, d
   }
 }
 
-// (mean, rstd) from partial (sum, sumsq) records summed in record order; torch: biased variance,
-// rstd = 1/sqrt(max(var,0)+eps).
-__device__ __forceinline__ void slots_stats(const double* p, int n, int stride, double count, float eps,
-                                            float& mean, float& rstd) {
-  double s = 0.0, ss = 0.0;
-  for (int i = 0; i < n; ++i) { s += p[(size_t)i * stride]; ss += p[(size_t)i * stride + 1]; }
-  const double mu = s / count;
-  double var = ss / count - mu * mu;
-  if (var < 0.0) var = 0.0;
-  mean = (float)mu;
-  rstd = (float)(1.0 / sqrt(var + (double)eps));
-}
-
 // x' for one element: o = X value, r = X2 value, g = a_f[k] * a_t[t] (1 when attention is off).
 template <int MODE>
 __device__ __forceinline__ float resid_apply(float o, float r, float g, int k, const float* c0, const float* c1,
@@ -87,75 +74,120 @@ __device__ __forceinline__ float resid_apply(float o, float r, float g, int k, c
 
 
 // ---- consumer-side statistics: partial records -> GroupNorm affine vectors in LDS --------------
-// Records are loaded by all threads in parallel into LDS and summed in record order (fixed =>
-// deterministic, identical in every consumer workgroup). All threads must call (barriers).
+// Phase 1 (reduce_records, no barrier): the values of up to two record sources are summed over
+// records, one value per wave (lane l takes records l, l+64, ...; then a fixed butterfly), so every
+// consumer workgroup derives bitwise identical statistics. All loads are issued before any
+// reduction. Phase 2 (after a barrier): per-channel affines from the sums, with gamma/beta
+// prefetched into registers before phase 1 (ld_chan).
 
-// Sum nrec records (stride rs, values at [off, off+nv)) into out[0..nv) (LDS). Thread (g, j) sums
-// value j over records g, g+G, ... in order, then thread j sums the G partials in order.
-// tmp: >= blockDim doubles of LDS.
-__device__ inline void sum_records(const double* rec, int nrec, int rs, int off, int nv, double* tmp, double* out) {
-  const int G = blockDim.x / nv;
-  const int t = threadIdx.x;
-  if (t < G * nv) {
-    const int g = t / nv, j = t % nv;
-    double s = 0.0;
-    for (int r = g; r < nrec; r += G) s += rec[(size_t)r * rs + off + j];
-    tmp[t] = s;
+struct RecSrc {
+  const double* p;  // first value of utterance b's first record
+  int n, rs, nv;    // records, record stride (doubles), values per record used
+};
+
+__device__ __forceinline__ RecSrc rec_src(const GnSrc& s, int b, int nv) {
+  return RecSrc{s.rec + (size_t)b * s.nrec * s.rstride + s.roff, s.nrec, s.rstride, nv};
+}
+__device__ __forceinline__ RecSrc rec_none() { return RecSrc{nullptr, 0, 0, 0}; }
+
+// out[j] for j < s0.nv + s1.nv (<= 4 * waves): sums of value j (s0's values first).
+__device__ inline void reduce_records(const RecSrc& s0, const RecSrc& s1, double* out) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int nv = s0.nv + s1.nv;
+  double v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = w + nw * i;
+    v[i] = 0.0;
+    if (j < nv) {
+      const bool f = j < s0.nv;
+      const double* p = f ? s0.p + j : s1.p + (j - s0.nv);
+      const int n = f ? s0.n : s1.n, rs = f ? s0.rs : s1.rs;
+      if (l < n) v[i] = p[(size_t)l * rs];
+      for (int r = l + 64; r < n; r += 64) v[i] += p[(size_t)r * rs];
+    }
   }
-  __syncthreads();
-  if (t < nv) {
-    double s = 0.0;
-    for (int g = 0; g < G; ++g) s += tmp[g * nv + t];
-    out[t] = s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = w + nw * i;
+    if (j < nv) {
+      const double s = wave_sum(v[i]);
+      if (l == 0) out[j] = s;
+    }
   }
-  __syncthreads();
 }
 
-// GroupNorm(1,K) affine (scale s[k], shift h[k]) of utterance b from its (sum, sumsq) records.
-__device__ inline void gn_from_records(const GnSrc& src, int b, int K, int T, float* s, float* h, double* tmp,
-                                       double* acc) {
-  sum_records(src.rec + (size_t)b * src.nrec * src.rstride, src.nrec, src.rstride, src.roff, 2, tmp, acc);
-  const double cnt = (double)K * T;
-  const double mu = acc[0] / cnt;
-  double var = acc[1] / cnt - mu * mu;
+// Per-channel parameters of channels k = tid, tid + blockDim (K <= 2 * blockDim) into registers.
+__device__ __forceinline__ void ld_chan(const float* p, int K, float (&r)[2]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = threadIdx.x + q * blockDim.x;
+    r[q] = k < K ? p[k] : 0.f;
+  }
+}
+
+// (mean, rstd) as torch computes GroupNorm(1, K) statistics: biased variance, 1/sqrt(var + eps).
+__device__ __forceinline__ void gn_moments(double s, double ss, double cnt, float eps, float& mu, float& rstd) {
+  const double m = s / cnt;
+  double var = ss / cnt - m * m;
   if (var < 0.0) var = 0.0;
-  const float muf = (float)mu, rs = (float)(1.0 / sqrt(var + (double)src.eps));
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const float sc = rs * src.g[k];
-    s[k] = sc;
-    h[k] = src.be[k] - sc * muf;
+  mu = (float)m;
+  rstd = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// GroupNorm affine from acc = {sum, sumsq}: s[k] = rstd*g[k], h[k] = be[k] - s[k]*mean.
+__device__ __forceinline__ void gn_affine(const double* acc, int K, int T, float eps, const float (&g)[2],
+                                          const float (&be)[2], float* s, float* h) {
+  float mu, rs;
+  gn_moments(acc[0], acc[1], (double)K * T, eps, mu, rs);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = threadIdx.x + q * blockDim.x;
+    if (k < K) {
+      const float sc = rs * g[q];
+      s[k] = sc;
+      h[k] = be[q] - sc * mu;
+    }
   }
 }
 
-// Recursive-LN affine (GN_a: sa, ha; GN_b: sb, hb) of utterance b from the moment records
+// Recursive-LN affines (GN_a: c0, c1; GN_b: c2, c3) from the moment sums
 //   0 Σo  1 Σo²  2 Σu  3 Σu²  4 Σbe·o  5 Σg·u  6 Σg·o·u  7 Σg·o  8 Σg·be·u  9 Σg²·u²  10 Σg²·u
 // (u = o + r', g = gamma_a[c], be = beta_a[c]); v = (o+be) + ra·g·(u-μa) gives Σv, Σv² in closed
 // form, so neither u nor v is materialized. wsum = {Σg, Σbe, Σbe², Σg·be, Σg²} over channels (host).
-__device__ inline void recursive_from_records(const LoadSpec& ld, int b, int K, int T, float* c0, float* c1,
-                                              float* c2, float* c3, double* tmp, double* acc) {
-  sum_records(ld.gn.rec + (size_t)b * ld.gn.nrec * NMOM, ld.gn.nrec, NMOM, 0, NMOM, tmp, acc);
-  const double* m = acc;
+__device__ inline void recursive_affine(const double* m, const LoadSpec& ld, int K, int T, const float (&ga)[2],
+                                        const float (&ba)[2], const float (&gb)[2], const float (&bb)[2], float* c0,
+                                        float* c1, float* c2, float* c3) {
   const double cnt = (double)K * T, Tn = (double)T;
-  const double mua = m[2] / cnt;
-  double vara = m[3] / cnt - mua * mua;
-  if (vara < 0.0) vara = 0.0;
-  const float rsa = (float)(1.0 / sqrt(vara + (double)ld.gn.eps));
-  const float mua_f = (float)mua;
+  float mua_f, rsa;
+  gn_moments(m[2], m[3], cnt, ld.gn.eps, mua_f, rsa);
   const double ra = rsa, mu = mua_f;
   const double gs = ld.wsum[0], bs = ld.wsum[1], bbs = ld.wsum[2], gbs = ld.wsum[3], ggs = ld.wsum[4];
   const double sv = m[0] + ra * (m[5] - mu * Tn * gs) + Tn * bs;
   const double svv = m[1] + 2.0 * m[4] + Tn * bbs + 2.0 * ra * (m[6] - mu * m[7] + m[8] - mu * Tn * gbs) +
                      ra * ra * (m[9] - 2.0 * mu * m[10] + mu * mu * Tn * ggs);
-  const double mub = sv / cnt;
-  double varb = svv / cnt - mub * mub;
-  if (varb < 0.0) varb = 0.0;
-  const float mub_f = (float)mub, rsb = (float)(1.0 / sqrt(varb + (double)ld.eps2));
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const float sa = rsa * ld.gn.g[k];
-    c0[k] = sa; c1[k] = ld.gn.be[k] - sa * mua_f;
-    const float sb = rsb * ld.g2[k];
-    c2[k] = sb; c3[k] = ld.be2[k] - sb * mub_f;
+  float mub_f, rsb;
+  gn_moments(sv, svv, cnt, ld.eps2, mub_f, rsb);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = threadIdx.x + q * blockDim.x;
+    if (k < K) {
+      const float sa = rsa * ga[q];
+      c0[k] = sa; c1[k] = ba[q] - sa * mua_f;
+      const float sb = rsb * gb[q];
+      c2[k] = sb; c3[k] = bb[q] - sb * mub_f;
+    }
   }
+}
+
+// Single-source convenience form (one barrier inside; all threads must call).
+__device__ inline void gn_from_records(const GnSrc& src, int b, int K, int T, float* s, float* h, double* acc) {
+  float g[2], be[2];
+  ld_chan(src.g, K, g);
+  ld_chan(src.be, K, be);
+  reduce_records(rec_src(src, b, 2), rec_none(), acc);
+  __syncthreads();
+  gn_affine(acc, K, T, src.eps, g, be, s, h);
 }
 
 }  // namespace sepvad

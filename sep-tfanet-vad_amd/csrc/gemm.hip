@@ -14,8 +14,8 @@
 //               Products of fp16 are exact in fp32, so only the dropped lo*lo term (~2^-22 relative)
 //               and fp32 accumulation remain: parity matches the fp32 path (tests/test_gpu_parity.py).
 //   PREC_F32:   v_mfma_f32_32x32x2_f32 (exact fp32 fma chain), 1/16 of the f16 MFMA rate.
-// Tile 64 frames x 64 channels, K chunk 32, 4 waves (2x2), one 32x32 accumulator per wave;
-// register-staged double-buffered LDS, one barrier per K chunk.
+// Tile 64 frames x 64 channels, K chunk 64, 4 waves (2x2), one 32x32 accumulator per wave;
+// single-buffered LDS with the next chunk prefetched into registers while the MFMAs run.
 #include "device_common.h"
 
 namespace sepvad {
@@ -25,17 +25,22 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BT = 64;        // frames per tile
 constexpr int BMC = 64;       // output channels per tile
-constexpr int BK = 32;        // K chunk
-constexpr int LDH = BK + 8;   // halves per LDS row: 80 B rows make the 16-B fragment reads conflict-free
+constexpr int BK = 64;        // K chunk
+constexpr int LDH = BK + 8;   // halves per LDS row: 144 B = 9 x 16 B (odd) => conflict-free 16-B fragment reads
 constexpr int LDF = BK + 1;   // floats per LDS row (fp32 path)
 constexpr int KMAX = 512;
 constexpr int DWROWS = BT + 8;  // LD_DW halo rows (dilation <= 4)
+constexpr int NA = BT * BK / 4 / 256;          // float4 of the A chunk per thread (4)
+constexpr int NDW = (DWROWS * BK / 2 / 4 + 255) / 256;  // float4 of the LD_DW halo chunk per thread (3)
+constexpr int NWH = BMC * BK / 8 / 256;        // uint4 (8 halves) of each W split per thread (2)
+constexpr int NWF = BMC * BK / 4 / 256;        // float4 of the fp32 W chunk per thread (4)
 
+// Single-buffered LDS tiles; the next chunk is prefetched into registers during the MFMAs.
 struct SmemF16 {
-  __half Ahi[2][BT][LDH], Alo[2][BT][LDH], Bhi[2][BMC][LDH], Blo[2][BMC][LDH];
+  __half Ahi[BT][LDH], Alo[BT][LDH], Bhi[BMC][LDH], Blo[BMC][LDH];
 };
 struct SmemF32 {
-  float A[2][BT][LDF], B[2][BMC][LDF];
+  float A[BT][LDF], B[BMC][LDF];
 };
 
 __device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
@@ -59,9 +64,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   __shared__ float afk[(LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) ? KMAX : 1];
   __shared__ float atr[BT];
   __shared__ float wdl[LM == LD_DW ? HID * 4 : 1];  // dconv taps (3) + bias per output channel
-  __shared__ float Hs[LM == LD_DW ? DWROWS : 1][LM == LD_DW ? 17 : 1];
-  __shared__ double dtmp[256];
-  __shared__ double dacc[NMOM];
+  __shared__ float Hs[LM == LD_DW ? DWROWS : 1][LM == LD_DW ? BK / 2 + 1 : 1];
+  __shared__ double dacc[16];
   __shared__ float epi[2][2][64];
 
   const int tid = threadIdx.x;
@@ -75,18 +79,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   const LoadSpec& ld = a.ld;
 
   // ---------------- staging: global -> registers -> (transform) -> LDS ----------------
-  float4 ro[2], rr[2];
-  uint4 whr, wlr;
-  float4 wf[2];
+  float4 ro[LM == LD_DW ? NDW : NA], rr[NA];
+  static_assert(NWH == 2, "W prefetch registers are named, not an array (keeps them out of scratch)");
+  uint4 wh0, wh1, wl0, wl1;
+  float4 wf[NWF];
   const size_t arow0 = (size_t)b * Tp + t0;
 
   auto gather = [&](int k0) {
     if constexpr (LM == LD_DW) {
       const int c0 = k0 >> 1;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NDW; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 2, q = idx & 3;
+        const int row = idx >> 3, q = idx & 7;
         const int t = t0 - ld.dil + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (row < BT + 2 * ld.dil && t >= 0 && t < T)
@@ -95,9 +100,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NA; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
         const size_t off = (arow0 + row) * K + k0 + c4;
         ro[i] = *reinterpret_cast<const float4*>(ld.X + off);
         if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD)
@@ -105,28 +110,31 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
       }
     }
     if constexpr (PREC == PREC_F16X3) {
-      const int row = tid >> 2, q = tid & 3;
-      whr = *reinterpret_cast<const uint4*>(a.Whi + (size_t)(m0 + row) * K + k0 + 8 * q);
-      wlr = *reinterpret_cast<const uint4*>(a.Wlo + (size_t)(m0 + row) * K + k0 + 8 * q);
+      const int row = tid >> 3, q = tid & 7;
+      const size_t o0 = (size_t)(m0 + row) * K + k0 + 8 * q, o1 = o0 + (size_t)32 * K;
+      wh0 = *reinterpret_cast<const uint4*>(a.Whi + o0);
+      wh1 = *reinterpret_cast<const uint4*>(a.Whi + o1);
+      wl0 = *reinterpret_cast<const uint4*>(a.Wlo + o0);
+      wl1 = *reinterpret_cast<const uint4*>(a.Wlo + o1);
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NWF; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
         wf[i] = *reinterpret_cast<const float4*>(a.W32 + (size_t)(m0 + row) * K + k0 + c4);
       }
     }
   };
 
-  auto put_a = [&](int buf, int row, int col, const float4& v) {  // 4 consecutive k at (row, col)
+  auto put_a = [&](int row, int col, const float4& v) {  // 4 consecutive k at (row, col)
     if constexpr (PREC == PREC_F16X3) {
       uint2 hi, lo;
       split4(v, hi, lo);
-      *reinterpret_cast<uint2*>(&sm.Ahi[buf][row][col]) = hi;
-      *reinterpret_cast<uint2*>(&sm.Alo[buf][row][col]) = lo;
+      *reinterpret_cast<uint2*>(&sm.Ahi[row][col]) = hi;
+      *reinterpret_cast<uint2*>(&sm.Alo[row][col]) = lo;
     } else {
-      sm.A[buf][row][col + 0] = v.x; sm.A[buf][row][col + 1] = v.y;
-      sm.A[buf][row][col + 2] = v.z; sm.A[buf][row][col + 3] = v.w;
+      sm.A[row][col + 0] = v.x; sm.A[row][col + 1] = v.y;
+      sm.A[row][col + 2] = v.z; sm.A[row][col + 3] = v.w;
     }
   };
 
@@ -135,14 +143,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
     else return x;
   };
 
-  auto stage = [&](int buf, int k0) {
+  auto stage = [&](int k0) {
     if constexpr (LM == LD_DW) {
       // 1) normalized a (GN1) of the halo rows into Hs[row][c_local], zero outside [0, T)
       const int c0 = k0 >> 1;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NDW; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 2, q = idx & 3;
+        const int row = idx >> 3, q = idx & 7;
         if (row < BT + 2 * ld.dil) {
           const int t = t0 - ld.dil + row;
           const bool ok = t >= 0 && t < T;
@@ -155,28 +163,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
         }
       }
       __syncthreads();
-      // 2) d = PReLU(dconv) for 64 rows x 32 output channels, then GN2 -> A tile
-      const int row = tid >> 2, jg = (tid & 3) * 8;
+      // 2) d = PReLU(dconv) for 64 rows x 64 output channels, then GN2 -> A tile
+      const int row = tid >> 2, jg = (tid & 3) * 16;
       const int dl = ld.dil;
-      float dv[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int jl = jg + jj, j = k0 + jl, cl = jl >> 1;
-        const float* w = &wdl[j * 4];
-        float v = w[3];
-        v = fmaf(w[0], Hs[row][cl], v);
-        v = fmaf(w[1], Hs[row + dl][cl], v);
-        v = fmaf(w[2], Hs[row + 2 * dl][cl], v);
-        v = prelu_f(v, ld.alpha_d);
-        dv[jj] = fmaf(v, cf[0][j], cf[1][j]);
+      for (int h = 0; h < 4; ++h) {
+        float dv[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int jl = jg + 4 * h + jj, j = k0 + jl, cl = jl >> 1;
+          const float* w = &wdl[j * 4];
+          float v = w[3];
+          v = fmaf(w[0], Hs[row][cl], v);
+          v = fmaf(w[1], Hs[row + dl][cl], v);
+          v = fmaf(w[2], Hs[row + 2 * dl][cl], v);
+          v = prelu_f(v, ld.alpha_d);
+          dv[jj] = fmaf(v, cf[0][j], cf[1][j]);
+        }
+        put_a(row, jg + 4 * h, make_float4(dv[0], dv[1], dv[2], dv[3]));
       }
-      put_a(buf, row, jg, make_float4(dv[0], dv[1], dv[2], dv[3]));
-      put_a(buf, row, jg + 4, make_float4(dv[4], dv[5], dv[6], dv[7]));
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NA; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 3, c4 = (idx & 7) * 4;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
         const int k = k0 + c4;
         float4 v = ro[i];
         if constexpr (LM != LD_PLAIN) {
@@ -198,20 +208,22 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
           v.x = head_apply(v.x, k); v.y = head_apply(v.y, k + 1);
           v.z = head_apply(v.z, k + 2); v.w = head_apply(v.w, k + 3);
         }
-        put_a(buf, row, c4, v);
+        put_a(row, c4, v);
       }
     }
     if constexpr (PREC == PREC_F16X3) {
-      const int row = tid >> 2, q = tid & 3;
-      *reinterpret_cast<uint4*>(&sm.Bhi[buf][row][8 * q]) = whr;
-      *reinterpret_cast<uint4*>(&sm.Blo[buf][row][8 * q]) = wlr;
+      const int row = tid >> 3, q = tid & 7;
+      *reinterpret_cast<uint4*>(&sm.Bhi[row][8 * q]) = wh0;
+      *reinterpret_cast<uint4*>(&sm.Bhi[row + 32][8 * q]) = wh1;
+      *reinterpret_cast<uint4*>(&sm.Blo[row][8 * q]) = wl0;
+      *reinterpret_cast<uint4*>(&sm.Blo[row + 32][8 * q]) = wl1;
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NWF; ++i) {
         const int idx = tid + 256 * i;
-        const int row = idx >> 3, c4 = (idx & 7) * 4;
-        sm.B[buf][row][c4 + 0] = wf[i].x; sm.B[buf][row][c4 + 1] = wf[i].y;
-        sm.B[buf][row][c4 + 2] = wf[i].z; sm.B[buf][row][c4 + 3] = wf[i].w;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
+        sm.B[row][c4 + 0] = wf[i].x; sm.B[row][c4 + 1] = wf[i].y;
+        sm.B[row][c4 + 2] = wf[i].z; sm.B[row][c4 + 3] = wf[i].w;
       }
     }
   };
@@ -223,51 +235,81 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   const int nk = K / BK;
   gather(0);
   // ---------------- prologue (overlaps the first chunk's loads): GN affines -> LDS ----------------
-  if constexpr (LM == LD_GN || LM == LD_RESIDUAL) gn_from_records(ld.gn, b, K, T, cf[0], cf[1], dtmp, dacc);
-  if constexpr (LM == LD_RECURSIVE) recursive_from_records(ld, b, K, T, cf[0], cf[1], cf[2], cf[3], dtmp, dacc);
-  if constexpr (LM == LD_DW) {
-    gn_from_records(ld.gd1, b, CH, T, cf[2], cf[3], dtmp, dacc);  // GN1 (reg1) over a
-    gn_from_records(ld.gn, b, HID, T, cf[0], cf[1], dtmp, dacc);  // GN2 (reg2) over d
-    for (int j = tid; j < HID; j += 256) {
-      wdl[j * 4 + 0] = ld.wd[j * 3 + 0];
-      wdl[j * 4 + 1] = ld.wd[j * 3 + 1];
-      wdl[j * 4 + 2] = ld.wd[j * 3 + 2];
-      wdl[j * 4 + 3] = ld.bd[j];
+  // all record / parameter loads are issued before the single reduction barrier
+  {
+    RecSrc s0 = rec_none(), s1 = rec_none();
+    float p0[2], p1[2], p2[2], p3[2], p4[2], p5[2];
+    if constexpr (LM == LD_GN || LM == LD_RESIDUAL) {
+      s0 = rec_src(ld.gn, b, 2);
+      ld_chan(ld.gn.g, K, p0); ld_chan(ld.gn.be, K, p1);
     }
-  }
-  if constexpr (HEAD) gn_from_records(ld.gh, b, K, T, hco[0], hco[1], dtmp, dacc);
-  if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
-    for (int k = tid; k < K; k += 256) afk[k] = ld.af ? ld.af[(size_t)b * K + k] : 1.f;
-    if (tid < BT) atr[tid] = ld.at ? ld.at[(size_t)b * Tp + t0 + tid] : 1.f;
+    if constexpr (LM == LD_RECURSIVE) {
+      s0 = rec_src(ld.gn, b, NMOM);
+      ld_chan(ld.gn.g, K, p0); ld_chan(ld.gn.be, K, p1);
+      ld_chan(ld.g2, K, p2); ld_chan(ld.be2, K, p3);
+    }
+    if constexpr (LM == LD_DW) {
+      s0 = rec_src(ld.gd1, b, 2);  // GN1 (reg1) over a
+      s1 = rec_src(ld.gn, b, 2);   // GN2 (reg2) over d
+      ld_chan(ld.gd1.g, CH, p0); ld_chan(ld.gd1.be, CH, p1);
+      ld_chan(ld.gn.g, HID, p2); ld_chan(ld.gn.be, HID, p3);
+    }
+    if constexpr (HEAD) {
+      s1 = rec_src(ld.gh, b, 2);
+      ld_chan(ld.gh.g, K, p4); ld_chan(ld.gh.be, K, p5);
+    }
+    reduce_records(s0, s1, dacc);
+    if constexpr (LM == LD_DW) {
+      for (int j = tid; j < HID; j += 256) {
+        wdl[j * 4 + 0] = ld.wd[j * 3 + 0];
+        wdl[j * 4 + 1] = ld.wd[j * 3 + 1];
+        wdl[j * 4 + 2] = ld.wd[j * 3 + 2];
+        wdl[j * 4 + 3] = ld.bd[j];
+      }
+    }
+    if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD) {
+      for (int k = tid; k < K; k += 256) afk[k] = ld.af ? ld.af[(size_t)b * K + k] : 1.f;
+      if (tid < BT) atr[tid] = ld.at ? ld.at[(size_t)b * Tp + t0 + tid] : 1.f;
+    }
+    __syncthreads();
+    if constexpr (LM == LD_GN || LM == LD_RESIDUAL) gn_affine(dacc, K, T, ld.gn.eps, p0, p1, cf[0], cf[1]);
+    if constexpr (LM == LD_RECURSIVE) recursive_affine(dacc, ld, K, T, p0, p1, p2, p3, cf[0], cf[1], cf[2], cf[3]);
+    if constexpr (LM == LD_DW) {
+      gn_affine(dacc, CH, T, ld.gd1.eps, p0, p1, cf[2], cf[3]);
+      gn_affine(dacc + 2, HID, T, ld.gn.eps, p2, p3, cf[0], cf[1]);
+    }
+    if constexpr (HEAD) gn_affine(dacc + s0.nv, K, T, ld.gh.eps, p4, p5, hco[0], hco[1]);
   }
   __syncthreads();
 
-  stage(0, 0);
+  stage(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
     if (kt + 1 < nk) gather((kt + 1) * BK);
     if constexpr (PREC == PREC_F16X3) {
       const int ar = wr * 32 + (lane & 31), br = wc * 32 + (lane & 31), kh = 8 * (lane >> 5);
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
-        const half8 ah = *reinterpret_cast<const half8*>(&sm.Ahi[buf][ar][16 * s + kh]);
-        const half8 al = *reinterpret_cast<const half8*>(&sm.Alo[buf][ar][16 * s + kh]);
-        const half8 bh = *reinterpret_cast<const half8*>(&sm.Bhi[buf][br][16 * s + kh]);
-        const half8 bl = *reinterpret_cast<const half8*>(&sm.Blo[buf][br][16 * s + kh]);
+        const half8 ah = *reinterpret_cast<const half8*>(&sm.Ahi[ar][16 * s + kh]);
+        const half8 al = *reinterpret_cast<const half8*>(&sm.Alo[ar][16 * s + kh]);
+        const half8 bh = *reinterpret_cast<const half8*>(&sm.Bhi[br][16 * s + kh]);
+        const half8 bl = *reinterpret_cast<const half8*>(&sm.Blo[br][16 * s + kh]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
       }
     } else {
-      const float* Ab = &sm.A[buf][wr * 32 + (lane & 31)][lane >> 5];
-      const float* Bb = &sm.B[buf][wc * 32 + (lane & 31)][lane >> 5];
+      const float* Ab = &sm.A[wr * 32 + (lane & 31)][lane >> 5];
+      const float* Bb = &sm.B[wc * 32 + (lane & 31)][lane >> 5];
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ab[kk], Bb[kk], acc, 0, 0, 0);
     }
-    if (kt + 1 < nk) stage(buf ^ 1, (kt + 1) * BK);
     __syncthreads();
+    if (kt + 1 < nk) {
+      stage((kt + 1) * BK);
+      __syncthreads();
+    }
   }
 
   // ---------------- epilogue: lane = column m, registers = rows t ----------------

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   __shared__ float vadv[IS_FR + 4];           // vad at frames fbeg-2 .. fbeg+IS_FR+1
   __shared__ float gain[IS_FR];
   __shared__ float vs[4], vh[4];
-  __shared__ double dtmp[512], dacc[2];
+  __shared__ double dacc[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bs = blockIdx.x, f0 = blockIdx.y * IS_OWN;
   const int T = a.T;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
 
   // 0) VAD tail for the frames this block needs
   if (a.est_mode && a.has_vad) {
-    gn_from_records(a.vgn, bs, 4, T, vs, vh, dtmp, dacc);  // BN_1 = GroupNorm(1, 4, eps 1e-8)
+    gn_from_records(a.vgn, bs, 4, T, vs, vh, dacc);  // BN_1 = GroupNorm(1, 4, eps 1e-8)
     __syncthreads();
     if (tid < 4 * (IS_FR + 6)) {
       const int o = tid / (IS_FR + 6), q = tid % (IS_FR + 6);

@@ -10,7 +10,7 @@
 //   k_head_stats  statistics of PReLU(o_final) (model/model.py:322-325) for TCN.output.1
 // Workgroup = (utterance, a few frames), thread = channel: every row access is a coalesced 1 KB read.
 // Each workgroup writes one partial record (deterministic, no atomics); consumers turn the records
-// into GroupNorm affines in their prologues (device_common.h gn_from_records / recursive_from_records).
+// into GroupNorm affines in their prologues (device_common.h reduce_records + gn_affine / recursive_affine).
 #include "device_common.h"
 
 namespace sepvad {
@@ -77,15 +77,23 @@ __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
   __shared__ float H[R + 8][CH];   // GN1(a) rows t0-dil .. t0+R+dil (zero outside [0,T))
   __shared__ float red[2 * 16];
   __shared__ float s1[CH], h1[CH];
-  __shared__ double dtmp[256], dacc[2];
+  __shared__ double dacc[2];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const int T = a.T, dl = a.dil;
-  gn_from_records(a.gd1, b, CH, T, s1, h1, dtmp, dacc);
-  const float sc = s1[c], sh = h1[c];
-  for (int rr = 0; rr < R + 2 * dl; ++rr) {
+  // issue the row loads first: their latency overlaps the record reduction below
+  float raw[R + 8];
+#pragma unroll
+  for (int rr = 0; rr < R + 8; ++rr) {
     const int t = t0 - dl + rr;
-    H[rr][c] = (t >= 0 && t < T) ? fmaf(a.A[((size_t)b * a.Tp + t) * CH + c], sc, sh) : 0.f;
+    raw[rr] = (rr < R + 2 * dl && t >= 0 && t < T) ? a.A[((size_t)b * a.Tp + t) * CH + c] : 0.f;
+  }
+  gn_from_records(a.gd1, b, CH, T, s1, h1, dacc);
+  const float sc = s1[c], sh = h1[c];
+#pragma unroll
+  for (int rr = 0; rr < R + 8; ++rr) {
+    const int t = t0 - dl + rr;
+    if (rr < R + 2 * dl) H[rr][c] = (t >= 0 && t < T) ? fmaf(raw[rr], sc, sh) : 0.f;
   }
   // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2); own column only
   float st[2] = {0.f, 0.f};
@@ -122,6 +130,16 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const int T = a.T;
+  const bool rec = a.ln_mode == LD_RECURSIVE;
+  // issue the row loads first: their latency overlaps the gate computation below
+  float rv[R], ov[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int t = t0 + i;
+    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
+    rv[i] = t < T ? a.R[off] : 0.f;
+    ov[i] = (rec && t < T) ? a.O[off] : 0.f;
+  }
   float afc = 1.f;
   if (a.tf_att) {
     const float* p = a.attp;
@@ -166,19 +184,18 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
     if (c < R) a.at[(size_t)b * a.Tp + t0 + c] = ats[c];
   }
   // moment record over this workgroup's frames (t < T), see device_common.h finalize_recursive
-  const bool rec = a.ln_mode == LD_RECURSIVE;
   const float g = rec ? a.ga[c] : 0.f, be = rec ? a.bea[c] : 0.f;
   float m[NMOM];
 #pragma unroll
   for (int j = 0; j < NMOM; ++j) m[j] = 0.f;
+#pragma unroll
   for (int i = 0; i < R; ++i) {
     const int t = t0 + i;
     if (t >= T) break;
-    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
-    const float r = a.R[off];
+    const float r = rv[i];
     const float rp = a.tf_att ? r * (afc * ats[i]) : r;
     if (rec) {
-      const float o = a.O[off];
+      const float o = ov[i];
       const float u = o + rp;
       m[0] += o; m[1] += o * o; m[2] += u; m[3] += u * u; m[4] += be * o; m[5] += g * u;
       m[6] += g * o * u; m[7] += g * o; m[8] += g * be * u; m[9] += g * g * u * u; m[10] += g * g * u;
@@ -201,21 +218,37 @@ __global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
   constexpr int R = STAT_ROWS;
   __shared__ float red[2 * 16];
   __shared__ float cf[4][CH];
-  __shared__ double dtmp[256], dacc[NMOM];
+  __shared__ double dacc[NMOM];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const LoadSpec& ld = a.ld;
-  if (ld.mode == LD_RECURSIVE) recursive_from_records(ld, b, CH, a.T, cf[0], cf[1], cf[2], cf[3], dtmp, dacc);
-  else if (ld.mode == LD_RESIDUAL) gn_from_records(ld.gn, b, CH, a.T, cf[0], cf[1], dtmp, dacc);
+  float ov[R], rv[R], gt[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int t = t0 + i;
+    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
+    ov[i] = t < a.T ? ld.X[off] : 0.f;
+    rv[i] = t < a.T ? ld.X2[off] : 0.f;
+    gt[i] = (ld.at && t < a.T) ? ld.at[(size_t)b * a.Tp + t] : 1.f;
+  }
+  if (ld.mode == LD_RECURSIVE) {
+    float ga[2], ba[2], gb[2], bb[2];
+    ld_chan(ld.gn.g, CH, ga); ld_chan(ld.gn.be, CH, ba); ld_chan(ld.g2, CH, gb); ld_chan(ld.be2, CH, bb);
+    reduce_records(rec_src(ld.gn, b, NMOM), rec_none(), dacc);
+    __syncthreads();
+    recursive_affine(dacc, ld, CH, a.T, ga, ba, gb, bb, cf[0], cf[1], cf[2], cf[3]);
+  } else if (ld.mode == LD_RESIDUAL) {
+    gn_from_records(ld.gn, b, CH, a.T, cf[0], cf[1], dacc);
+  }
   __syncthreads();
   const float afc = ld.af ? ld.af[(size_t)b * CH + c] : 1.f;
   float st[2] = {0.f, 0.f};
+#pragma unroll
   for (int i = 0; i < R; ++i) {
     const int t = t0 + i;
     if (t >= a.T) break;
-    const size_t off = ((size_t)b * a.Tp + t) * CH + c;
-    const float o = ld.X[off], r = ld.X2[off];
-    const float g = afc * (ld.at ? ld.at[(size_t)b * a.Tp + t] : 1.f);
+    const float o = ov[i], r = rv[i];
+    const float g = afc * gt[i];
     float x;
     if (ld.mode == LD_RECURSIVE) x = resid_apply<LD_RECURSIVE>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]);
     else if (ld.mode == LD_RESIDUAL) x = resid_apply<LD_RESIDUAL>(o, r, g, c, cf[0], cf[1], cf[2], cf[3]);
