@@ -3,7 +3,7 @@
 //
 // Per forward (B utterances, T frames, 24 blocks):
 //   k_stft -> k_gate -> 24 x [ conv1d GEMM (loader: previous block's residual update)
-//                              -> k_dw_stats -> res_out GEMM (loader: GN1, dconv, PReLU, GN2)
+//                              -> k_dw_stats (d, split) -> res_out GEMM (reg2 folded into W / epilogue)
 //                              -> k_att_stats ]
 //   -> k_head_stats -> output GEMM (loader: residual update, PReLU, GN) -> k_vad1 -> k_istft
 #include <hip/hip_runtime.h>
@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -46,6 +47,7 @@ struct PackedW {
 struct BlockOff {
   PackedW w1, w2;
   size_t b1, g1, be1, wd, bd, b2, g2, be2, attp, lna_g, lna_b, lnb_g, lnb_b;
+  size_t fc2;  // res_out with reg2 folded in: w2 = W*gamma2, b2 = bias + W*beta2, fc2[m] = sum_k w2[m][k]
   float a1, a2;
   int dil;
   double wsum[5];  // {Σγa, Σβa, Σβa², Σγa·βa, Σγa²} of ln_first (closed-form recursive-LN stats)
@@ -57,6 +59,7 @@ struct Workspace {
   size_t bytes = 0;
   float2* X; float* specdb; float* S0; float* O[2]; float* A; float* R;
   float* masks; float* colsum; float* rowsum; float* at; float* af; float* vy; float* vad;
+  __half* Dhi; __half* Dlo; float* D32;  // res_out operand d (fp16 split planes, or fp32, same bytes)
   // partial records of the statistics producers (deterministic per-workgroup sums)
   double* rec_gate; double* rec_g1; double* rec_dw; double* rec_mom; double* rec_hs; double* rec_vad;
 };
@@ -86,6 +89,11 @@ struct sepvad_model {
   std::vector<hipEvent_t> ev;
   double gemm_ms = 0.0, g2_ms = 0.0, total_ms = 0.0;
   int gemm_launches = 0, g2_launches = 0;
+  // diagnostics: per-workgroup timestamps of one block's two GEMMs (env SEPVAD_PROBE_BLOCK=<i>,
+  // written to SEPVAD_PROBE_OUT after each forward)
+  int probe_blk = -1;
+  unsigned long long* probe = nullptr;
+  size_t probe_n = 0;
 
   const float* P(size_t off) const { return dparams + off; }
   const __half* H(size_t off) const { return dhalf + off; }
@@ -179,7 +187,7 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
   const size_t oX = take(bt * NBIN * 8), oSpec = take(bt * SPEC_LD * 4), oS0 = take(bt * CH * 4);
   const size_t oO0 = take(bt * CH * 4), oO1 = take(bt * CH * 4), oA = take(bt * CH * 4), oR = take(bt * CH * 4);
-  const size_t oM = take(bt * MOUT_PAD * 4);
+  const size_t oM = take(bt * MOUT_PAD * 4), oD = take(bt * HID * 4);
   const size_t oCs = take(bt * (CH / TILE) * 4), oRs = take((size_t)Bm * (Tm / TILE) * CH * 4);
   const size_t oAt = take(bt * 4), oAf = take((size_t)Bm * CH * 4), oVy = take(bt * 2 * 4 * 4), oV = take(bt * 2 * 4);
   const size_t oRg = take(bt / GATE_ROWS * 16 + 16), oR1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
@@ -193,6 +201,7 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   w.X = (float2*)(base + oX); w.specdb = (float*)(base + oSpec); w.S0 = (float*)(base + oS0);
   w.O[0] = (float*)(base + oO0); w.O[1] = (float*)(base + oO1); w.A = (float*)(base + oA);
   w.R = (float*)(base + oR); w.masks = (float*)(base + oM);
+  w.Dhi = (__half*)(base + oD); w.Dlo = w.Dhi + bt * HID; w.D32 = (float*)(base + oD);
   w.colsum = (float*)(base + oCs); w.rowsum = (float*)(base + oRs); w.at = (float*)(base + oAt);
   w.af = (float*)(base + oAf); w.vy = (float*)(base + oVy); w.vad = (float*)(base + oV);
   w.rec_gate = (double*)(base + oRg); w.rec_g1 = (double*)(base + oR1); w.rec_dw = (double*)(base + oRd);
@@ -341,8 +350,25 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     bo.be1 = pk.add(r1b, CH);
     bo.wd = pk.add(fold_wn(gd, vd, HID, 3));
     bo.bd = pk.add(bd, HID);
-    bo.w2 = pack_pointwise(pk, fold_wn(g2, v2, CH, HID), CH, HID, CH);
-    bo.b2 = pk.add(b2, CH);
+    {
+      // reg2 (GroupNorm(1, H) of d, model/model.py:136) folded out of the res_out operand: see gemm.hip
+      const std::vector<float> w2 = fold_wn(g2, v2, CH, HID);
+      std::vector<float> w2g((size_t)CH * HID), cb(CH), fc(CH);
+      for (int m = 0; m < CH; ++m) {
+        double sb = b2[m], sg = 0.0;
+        for (int k = 0; k < HID; ++k) {
+          const float wg = w2[(size_t)m * HID + k] * r2g[k];
+          w2g[(size_t)m * HID + k] = wg;
+          sg += wg;
+          sb += (double)w2[(size_t)m * HID + k] * r2b[k];
+        }
+        cb[m] = (float)sb;
+        fc[m] = (float)sg;
+      }
+      bo.w2 = pack_pointwise(pk, w2g, CH, HID, CH);
+      bo.b2 = pk.add(cb);
+      bo.fc2 = pk.add(fc);
+    }
     bo.g2 = pk.add(r2g, HID);
     bo.be2 = pk.add(r2b, HID);
     bo.a1 = a1[0];
@@ -495,6 +521,19 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
   h->ev.clear();
   std::vector<int> gemm_ev, g2_ev;
   if (ev_record(h, s)) return SEPVAD_E_HIP;
+  const size_t g1_grid = (size_t)B * ntu * (CH / TILE);
+  if (const char* pb = getenv("SEPVAD_PROBE_BLOCK")) {
+    h->probe_blk = atoi(pb);
+    const size_t need = 2 * g1_grid * PROBE_SLOTS;
+    if (need > h->probe_n) {
+      if (h->probe) (void)hipFree(h->probe);
+      h->probe = nullptr;
+      h->probe_n = 0;
+      HIPCHK(hipMalloc(&h->probe, need * sizeof(unsigned long long)));
+      h->probe_n = need;
+    }
+    HIPCHK(hipMemsetAsync(h->probe, 0, need * sizeof(unsigned long long), s));
+  }
 
   // 1. STFT (spec_input for the spectrum, spec_output for est; identical windows -> one pass)
   {
@@ -537,6 +576,7 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     g.Xmat = w.O[nxt];
     g.Y = w.A;
     g.out_rec = w.rec_g1;
+    if (i == h->probe_blk && h->probe) g.probe = h->probe;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
     if (ev_record(h, s)) return SEPVAD_E_HIP;
@@ -547,6 +587,7 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
     const GnSrc gn1 = gn_src(w.rec_g1, ntu * (CH / TILE), 2, 0, h->P(bo.g1), h->P(bo.be1), 1e-8f);
     d.gd1 = gn1; d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
+    d.prec = h->prec; d.Dhi = w.Dhi; d.Dlo = w.Dlo; d.D32 = w.D32;
     d.out_rec = w.rec_dw;
     HIPCHK(launch_dw_stats(d, s));
 
@@ -554,10 +595,15 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
     set_weights(h, g2, bo.w2);
     g2.bias = h->P(bo.b2);
-    g2.ld.mode = LD_DW; g2.ld.X = w.A; g2.ld.gd1 = gn1;
-    g2.ld.gn = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, h->P(bo.g2), h->P(bo.be2), 1e-8f);
-    g2.ld.wd = h->P(bo.wd); g2.ld.bd = h->P(bo.bd); g2.ld.alpha_d = bo.a2; g2.ld.dil = bo.dil;
+    if (h->prec == PREC_F16X3) {
+      g2.ld.mode = LD_SPLIT; g2.ld.Xh = w.Dhi; g2.ld.Xl = w.Dlo;
+    } else {
+      g2.ld.mode = LD_PLAIN; g2.ld.X = w.D32;
+    }
+    g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, 1e-8f);
+    g2.foldK = HID; g2.foldc = h->P(bo.fc2);
     g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
+    if (i == h->probe_blk && h->probe) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
     if (ev_record(h, s)) return SEPVAD_E_HIP;
@@ -634,6 +680,20 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     h->gemm_launches = (int)gemm_ev.size();
     h->g2_launches = (int)g2_ev.size();
   }
+  if (h->probe && h->probe_blk >= 0) {
+    const char* path = getenv("SEPVAD_PROBE_OUT");
+    std::vector<unsigned long long> hp(2 * g1_grid * PROBE_SLOTS);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(hp.data(), h->probe, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (path) {
+      if (FILE* f = fopen(path, "wb")) {
+        const long long hdr[4] = {(long long)g1_grid, PROBE_SLOTS, B, Tp};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+        fclose(f);
+      }
+    }
+  }
   return SEPVAD_OK;
 }
 
@@ -668,6 +728,7 @@ void sepvad_destroy(sepvad_handle h) {
   if (!h) return;
   DeviceGuard dg(h->device);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  if (h->probe) (void)hipFree(h->probe);
   if (h->ws.base) (void)hipFree(h->ws.base);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);

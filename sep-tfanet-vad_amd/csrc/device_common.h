@@ -74,11 +74,10 @@ __device__ __forceinline__ float resid_apply(float o, float r, float g, int k, c
 
 
 // ---- consumer-side statistics: partial records -> GroupNorm affine vectors in LDS --------------
-// Phase 1 (reduce_records, no barrier): the values of up to two record sources are summed over
-// records, one value per wave (lane l takes records l, l+64, ...; then a fixed butterfly), so every
-// consumer workgroup derives bitwise identical statistics. All loads are issued before any
-// reduction. Phase 2 (after a barrier): per-channel affines from the sums, with gamma/beta
-// prefetched into registers before phase 1 (ld_chan).
+// Phase 1 (reduce_records, no barrier): thread j sums value j of the record sources over their
+// records in record order (loads issued 16 at a time), so every consumer workgroup derives bitwise
+// identical statistics. Phase 2 (after a barrier): per-channel affines from the sums, with
+// gamma/beta prefetched into registers before phase 1 (ld_chan).
 
 struct RecSrc {
   const double* p;  // first value of utterance b's first record
@@ -90,31 +89,32 @@ __device__ __forceinline__ RecSrc rec_src(const GnSrc& s, int b, int nv) {
 }
 __device__ __forceinline__ RecSrc rec_none() { return RecSrc{nullptr, 0, 0, 0}; }
 
-// out[j] for j < s0.nv + s1.nv (<= 4 * waves): sums of value j (s0's values first).
+// out[j] for j < s0.nv + s1.nv (<= blockDim): sums of value j over records (s0's values first).
 __device__ inline void reduce_records(const RecSrc& s0, const RecSrc& s1, double* out) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int nv = s0.nv + s1.nv;
-  double v[4];
+  const int j = threadIdx.x;
+  if (j >= s0.nv + s1.nv) return;
+  const bool f = j < s0.nv;
+  const double* p = f ? s0.p + j : s1.p + (j - s0.nv);
+  const int n = f ? s0.n : s1.n;
+  const size_t rs = f ? s0.rs : s1.rs;
+  double s = 0.0;
+  int r = 0;
+  for (; r + 16 <= n; r += 16) {
+    double v[16];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = w + nw * i;
-    v[i] = 0.0;
-    if (j < nv) {
-      const bool f = j < s0.nv;
-      const double* p = f ? s0.p + j : s1.p + (j - s0.nv);
-      const int n = f ? s0.n : s1.n, rs = f ? s0.rs : s1.rs;
-      if (l < n) v[i] = p[(size_t)l * rs];
-      for (int r = l + 64; r < n; r += 64) v[i] += p[(size_t)r * rs];
-    }
-  }
+    for (int u = 0; u < 16; ++u) v[u] = p[(r + u) * rs];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = w + nw * i;
-    if (j < nv) {
-      const double s = wave_sum(v[i]);
-      if (l == 0) out[j] = s;
-    }
+    for (int u = 0; u < 16; ++u) s += v[u];
   }
+  for (; r + 4 <= n; r += 4) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = p[(r + u) * rs];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u];
+  }
+  for (; r < n; ++r) s += p[r * rs];
+  out[j] = s;
 }
 
 // Per-channel parameters of channels k = tid, tid + blockDim (K <= 2 * blockDim) into registers.
@@ -123,6 +123,32 @@ __device__ __forceinline__ void ld_chan(const float* p, int K, float (&r)[2]) {
   for (int q = 0; q < 2; ++q) {
     const int k = threadIdx.x + q * blockDim.x;
     r[q] = k < K ? p[k] : 0.f;
+  }
+}
+
+// Block reduction of NV per-thread floats through LDS (blockDim == 256, no shuffles): 16 threads
+// per value sum 16 slots each, then thread j sums the 16 partials in double (fixed order =>
+// deterministic) and stores out[j]. `lds` holds >= NV * 288 floats. Two barriers.
+template <int NV>
+__device__ inline void block_reduce_store_lds(float (&v)[NV], float* lds, double* out) {
+  const int t = threadIdx.x;
+  const int pos = (t >> 4) * 17 + (t & 15);  // rows of 16 padded to 17: conflict-free row sums
+#pragma unroll
+  for (int j = 0; j < NV; ++j) lds[j * 272 + pos] = v[j];
+  __syncthreads();
+  if (t < NV * 16) {
+    const int j = t >> 4, part = t & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += lds[j * 272 + part * 17 + u];
+    lds[NV * 272 + t] = s;
+  }
+  __syncthreads();
+  if (t < NV) {
+    double s = 0.0;
+#pragma unroll
+    for (int part = 0; part < 16; ++part) s += lds[NV * 272 + t * 16 + part];
+    out[t] = s;
   }
 }
 

@@ -23,6 +23,7 @@ constexpr int MOUT = 2 * NBIN;  // 514 output-head rows (2 speakers x 257 bins)
 constexpr int MOUT_PAD = 576;   // padded to a multiple of 64 (also the row stride of `masks`)
 constexpr int SPEC_LD = 260;    // row stride of the frame-major dB spectrum
 constexpr int STAT_ROWS = 8;    // rows (frames) per workgroup of the stats kernels
+constexpr int PROBE_SLOTS = 16;  // per-workgroup timestamps of a probed GEMM launch
 constexpr int NMOM = 11;        // moment record of k_att_stats (see device_common.h)
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
@@ -36,7 +37,7 @@ enum LoadMode {
   LD_RECURSIVE = 2,  // GN_b(o + GN_a(o + r'))   model/model.py:347-348 (stats: moment records)
   LD_RESIDUAL = 3,   // o + GN_c(r')             model/model.py:349-350 (stats of r': records)
   LD_ADD = 4,        // o + r'                   model/model.py:351-352
-  LD_DW = 5          // GN2(PReLU(dconv(GN1(a))))  model/model.py:132-136 (res_out operand)
+  LD_SPLIT = 5       // A already split into fp16 hi/lo planes (d from k_dw_stats; res_out operand)
 };
 // r' = r * (a_f[c] * a_t[t])  (TF_Attention, model/model.py:206-207), or r when tf_attention is off.
 
@@ -55,21 +56,19 @@ struct GnSrc {
 
 struct LoadSpec {
   int mode;
-  const float* X;        // [B][Tp][K]  o (or x, or a for LD_DW)
+  const float* X;        // [B][Tp][K]  o (or x)
   const float* X2;       // [B][Tp][K]  r (res_out output) for RECURSIVE/RESIDUAL/ADD
   const float* at;       // [B][Tp] time gate  (nullable => 1)
   const float* af;       // [B][K]  freq gate  (nullable => 1)
-  GnSrc gn;              // LD_GN: GN; LD_RESIDUAL: GN_c of r'; LD_RECURSIVE: GN_a (moment records);
-                         // LD_DW: GN2 (reg2) of d
+  const __half* Xh;      // LD_SPLIT: [B][Tp][K] fp16 hi plane
+  const __half* Xl;      // LD_SPLIT: [B][Tp][K] fp16 lo plane
+  GnSrc gn;              // LD_GN: GN; LD_RESIDUAL: GN_c of r'; LD_RECURSIVE: GN_a (moment records)
   const float* g2; const float* be2; float eps2;   // GN_b (recursive)
   double wsum[5];                                  // recursive: {Σg, Σbe, Σbe², Σg·be, Σg²} of GN_a
   // head: x' = GN_out(PReLU(transform(x)))  (model/model.py:322-325)
   int head;
   float alpha_h;
   GnSrc gh;
-  // LD_DW: a -> GN1 -> dconv (k=3, dilation dil, 2 outputs per input channel) -> PReLU
-  const float* wd; const float* bd; float alpha_d; int dil;
-  GnSrc gd1;             // GN1 (reg1) of a
 };
 
 struct GemmArgs {
@@ -87,13 +86,21 @@ struct GemmArgs {
   double* out_rec;      // EP_PRELU_STATS: [B][(Tp/64)*(M/64)][2] partial (sum, sumsq)
   float* colsum;        // EP_BIAS_ATT: [B][M/64][Tp]   partial sums over channels
   float* rowsum;        // EP_BIAS_ATT: [B][Tp/64][M]   partial sums over frames
+  // EP_BIAS_ATT: GroupNorm of the A operand folded out of the GEMM (gamma pre-multiplied into W):
+  // y = rstd * (acc - mu * foldc[m]) + bias[m]  with (mu, rstd) of `fold` over foldK x T values
+  GnSrc fold;
+  int foldK;
+  const float* foldc;   // [M] sum_k W'[m][k]
+  unsigned long long* probe;  // diagnostics (SEPVAD_PROBE_BLOCK): [grid][PROBE_SLOTS] wall-clock stamps
 };
 
-struct DwStatsArgs {     // statistics of d = PReLU(dconv(GN1(a))) for GN2 (reg2)
-  int B, T, Tp, dil;
+struct DwStatsArgs {     // d = PReLU(dconv(GN1(a))) (the res_out A operand) + its statistics for GN2 (reg2)
+  int B, T, Tp, dil, prec;
   const float* A;        // [B][Tp][CH]
   GnSrc gd1;             // GN1 (reg1) of a
   const float* wd; const float* bd; float alpha;
+  __half* Dhi; __half* Dlo;  // PREC_F16X3: [B][Tp][HID] split of d (rows >= T zero)
+  float* D32;            // PREC_F32: [B][Tp][HID] d
   double* out_rec;       // [B][Tp/STAT_ROWS][2]
 };
 

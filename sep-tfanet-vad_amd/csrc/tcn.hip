@@ -2,8 +2,9 @@
 //   k_gate        activity gate: Conv2d(1,1,3x3,pad 1) on the dB spectrum + PReLU, spectrum *= gate
 //                 (model/model.py:414-419); writes the TCN input (bins 1..256); TCN.LN statistics
 //                 (model/model.py:333,421) records
-//   k_dw_stats    statistics of d = PReLU(dconv(GN1(a))) (model/model.py:132-136) for reg2;
-//                 d itself is recomputed inside the res_out GEMM's operand loader and never stored
+//   k_dw_stats    d = PReLU(dconv(GN1(a))) (model/model.py:132-135), written once as the res_out
+//                 GEMM operand (fp16 hi/lo split for PREC_F16X3), and its statistics for reg2
+//                 (model/model.py:136), which the res_out epilogue folds in
 //   k_att_stats   TF_Attention gates a_t, a_f (model/model.py:197-205) from the res_out epilogue's partial
 //                 means, and the moment records of the residual update (model/model.py:345-350)
 //                 for the recursive/residual LN, without materializing u or v
@@ -88,6 +89,12 @@ __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
     const int t = t0 - dl + rr;
     raw[rr] = (rr < R + 2 * dl && t >= 0 && t < T) ? a.A[((size_t)b * a.Tp + t) * CH + c] : 0.f;
   }
+  float wv[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int j = 2 * c + q;
+    wv[q][0] = a.wd[j * 3 + 0]; wv[q][1] = a.wd[j * 3 + 1]; wv[q][2] = a.wd[j * 3 + 2]; wv[q][3] = a.bd[j];
+  }
   gn_from_records(a.gd1, b, CH, T, s1, h1, dacc);
   const float sc = s1[c], sh = h1[c];
 #pragma unroll
@@ -95,20 +102,30 @@ __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
     const int t = t0 - dl + rr;
     if (rr < R + 2 * dl) H[rr][c] = (t >= 0 && t < T) ? fmaf(raw[rr], sc, sh) : 0.f;
   }
-  // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2); own column only
+  // thread c owns input channel c -> output channels 2c, 2c+1 (groups=CH, multiplier 2); own column
+  // only, so no barrier is needed between the H writes and reads
   float st[2] = {0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int j = 2 * c + q;
-    const float w0 = a.wd[j * 3 + 0], w1 = a.wd[j * 3 + 1], w2 = a.wd[j * 3 + 2], bj = a.bd[j];
-    for (int i = 0; i < R; ++i) {
-      if (t0 + i >= T) break;
-      float v = bj;
-      v = fmaf(w0, H[i][c], v);
-      v = fmaf(w1, H[i + dl][c], v);
-      v = fmaf(w2, H[i + 2 * dl][c], v);
-      v = prelu_f(v, a.alpha);
-      st[0] += v; st[1] += v * v;
+  for (int i = 0; i < R; ++i) {
+    const int t = t0 + i;
+    float v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float x = wv[q][3];
+      x = fmaf(wv[q][0], H[i][c], x);
+      x = fmaf(wv[q][1], H[i + dl][c], x);
+      x = fmaf(wv[q][2], H[i + 2 * dl][c], x);
+      v[q] = t < T ? prelu_f(x, a.alpha) : 0.f;  // padding rows: zero operand rows for res_out
+      st[0] += v[q]; st[1] += v[q] * v[q];
+    }
+    const size_t off = ((size_t)b * a.Tp + t) * HID + 2 * c;
+    if (a.prec == PREC_F16X3) {
+      const __half h0 = __float2half_rn(v[0]), h1v = __float2half_rn(v[1]);
+      const __half l0 = __float2half_rn(v[0] - __half2float(h0)), l1 = __float2half_rn(v[1] - __half2float(h1v));
+      *reinterpret_cast<__half2*>(a.Dhi + off) = __halves2half2(h0, h1v);
+      *reinterpret_cast<__half2*>(a.Dlo + off) = __halves2half2(l0, l1);
+    } else {
+      *reinterpret_cast<float2*>(a.D32 + off) = make_float2(v[0], v[1]);
     }
   }
   const int nrec = a.Tp / R;
@@ -126,7 +143,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
   constexpr int R = STAT_ROWS;
   __shared__ float mT[CH + 8], yf[CH + 8];
   __shared__ float mC[R + 8], yt[R + 8], ats[R];
-  __shared__ float red[NMOM * 16];
+  __shared__ float red[NMOM * 288];
   const int b = blockIdx.x, t0 = blockIdx.y * R;
   const int c = threadIdx.x;
   const int T = a.T;
@@ -204,7 +221,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
     }
   }
   const int nrec = a.Tp / R;
-  block_reduce_store<NMOM>(m, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * NMOM);
+  block_reduce_store_lds<NMOM>(m, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * NMOM);
 }
 
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s) {
