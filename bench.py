@@ -46,6 +46,17 @@ def res_out_flops(B, T):
     return 2 * 256 * 512 * B * T
 
 
+def res_out_bytes(B, T):
+    """Compulsory bytes of one res_out launch: operand d as fp16 hi+lo planes (B*Tp x 512 x 4 B),
+    output r fp32 (B*Tp x 256 x 4 B), fp16 hi/lo weights (256 x 512 x 4 B)."""
+    Tp = (T + 63) // 64 * 64
+    return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
+
+
+PMC_FILE = "r01g_pmc_res_out.json"
+DEFAULT_SPLIT = 1
+
+
 def cpu_baseline(seconds: float = 12.0):
     """Oracle (CPU restatement, torch fp32) on the host: batches of the same workload until
     `seconds` of CPU work have elapsed (at least 2 batches)."""
@@ -78,6 +89,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=B_PER_GPU, help="utterances per GPU per step")
     ap.add_argument("--samples", type=int, default=N_SAMPLES)
+    ap.add_argument("--split", type=int, default=DEFAULT_SPLIT,
+                    help="concurrent utterance chunks per forward (internal streams; bitwise-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
@@ -115,6 +128,7 @@ def main():
     x = torch.from_numpy(x).to(dev)
     h = net.native_handle(dev)
     h.reserve(B, N)
+    h.set_split(args.split)
 
     def step():
         with torch.no_grad():
@@ -168,12 +182,15 @@ def main():
                                                  "v_mfma_f32_32x32x2_f32)")
         fwd_timed = n_gemm / (2 * 24 + 1)  # 49 GEMM launches per forward
         all_gemm_tflops = gemm_flops_per_utt(T) * B * fwd_timed / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
-        traffic = None
-        pmc = os.path.join(REPO, "profiles", "r01_pmc_res_out.json")
-        if os.path.exists(pmc):
+        # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
+        # (tools/gpu_round.sh -> tools/pmc.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
+        traffic = traffic_src = None
+        pmc = os.path.join(REPO, "profiles", PMC_FILE)
+        if os.path.exists(pmc) and args.precision == "f16x3" and B == B_PER_GPU and N == N_SAMPLES:
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-            except Exception:
+                traffic = round(json.load(open(pmc))["hbm_bytes_per_launch"])
+                traffic_src = "profiles/" + PMC_FILE
+            except (OSError, ValueError, KeyError):
                 traffic = None
         out = {
             "metric": METRIC,
@@ -188,6 +205,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "gemm_arithmetic": args.precision,
+            "split": args.split,
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
                     "recipe weights (pretrained .pth absent from the reference)",
             "config": {
@@ -206,6 +224,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": res_out_bytes(B, T),
                 "flops_per_launch": res_out_flops(B, T),
                 "avg_launch_us": round(res_avg_s * 1e6, 2),
                 "all_gemms_tflops": round(all_gemm_tflops, 3) if all_gemm_tflops else None,

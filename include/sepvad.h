@@ -102,6 +102,17 @@ int32_t sepvad_set_precision(sepvad_handle h, int32_t precision);
 int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N,
                        const SepVadOutputs* out, const SepVadInferKw* kw, void* stream);
 
+/* Same as sepvad_forward with a row stride: utterance b starts at x + b * ldx (ldx >= N).
+ * The streaming wrapper passes its overlapping windows this way (window k of stream b is
+ * x + b * N_total + k * hop, model/online_class_unknown_targets.py:39-41) without a gather copy. */
+int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int32_t B, int32_t N,
+                               const SepVadOutputs* out, const SepVadInferKw* kw, void* stream);
+
+/* Split each forward's batch into n (1..4) utterance chunks that run concurrently on internal
+ * streams forked from / joined to the caller's stream (results are bitwise identical for any n:
+ * every reduction is per utterance). Default 1, or the SEPVAD_SPLIT environment variable. */
+int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit);
+
 /* Front-end / back-end stages alone, for kernel-level parity tests:
  * STFT with DC zeroed (model/model.py:16-25,408-410) -> X [B, n_fft/2+1, T] complex64, and
  * 10 log10(clamp(|X|^2, 1e-10)) (model/model.py:411-412) -> spec [B, n_fft/2+1, T] (nullable). */

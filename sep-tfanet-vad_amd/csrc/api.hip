@@ -64,6 +64,28 @@ struct Workspace {
   double* rec_gate; double* rec_g1; double* rec_dw; double* rec_mom; double* rec_hs; double* rec_vad;
 };
 
+// The workspace slice of utterances [b0, b0 + Bc) at padded length Tp: every per-utterance array
+// is utterance-major, so a chunk is a pointer offset (no copies).
+Workspace ws_view(const Workspace& w, int b0, int Tp) {
+  Workspace v = w;
+  const size_t u = (size_t)b0 * Tp;
+  v.X = w.X + u * NBIN; v.specdb = w.specdb + u * SPEC_LD; v.S0 = w.S0 + u * CH;
+  v.O[0] = w.O[0] + u * CH; v.O[1] = w.O[1] + u * CH; v.A = w.A + u * CH; v.R = w.R + u * CH;
+  v.masks = w.masks + u * MOUT_PAD;
+  v.Dhi = w.Dhi + u * HID; v.Dlo = w.Dlo + u * HID; v.D32 = w.D32 + u * HID;
+  v.colsum = w.colsum + u * (CH / TILE); v.rowsum = w.rowsum + (size_t)b0 * (Tp / TILE) * CH;
+  v.at = w.at + u; v.af = w.af + (size_t)b0 * CH; v.vy = w.vy + u * 2 * 4; v.vad = w.vad + u * 2;
+  v.rec_gate = w.rec_gate + (size_t)b0 * (Tp / GATE_ROWS) * 2;
+  v.rec_g1 = w.rec_g1 + (size_t)b0 * (Tp / TILE) * (CH / TILE) * 2;
+  v.rec_dw = w.rec_dw + (size_t)b0 * (Tp / STAT_ROWS) * 2;
+  v.rec_mom = w.rec_mom + (size_t)b0 * (Tp / STAT_ROWS) * NMOM;
+  v.rec_hs = w.rec_hs + (size_t)b0 * (Tp / STAT_ROWS) * 2;
+  v.rec_vad = w.rec_vad + (size_t)b0 * 2 * (Tp / VAD_ROWS) * 2;
+  return v;
+}
+
+constexpr int MAX_SPLIT = 4;
+
 }  // namespace
 
 struct sepvad_model {
@@ -84,6 +106,11 @@ struct sepvad_model {
   size_t gate = 0;
   bool same_stft_window = true;
   Workspace ws;
+  // batch split: utterance chunks of one forward run concurrently on internal streams (fork/join
+  // on the caller's stream); the chunks' kernels fill each other's ramp/drain bubbles
+  int split = 1;
+  hipStream_t sub[MAX_SPLIT] = {};
+  hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;
@@ -246,19 +273,19 @@ GnSrc gn_src(const double* rec, int nrec, int rstride, int roff, const float* g,
   return s;
 }
 
-LoadSpec residual_spec(const sepvad_model* h, int i, const float* O, const float* R, int Tp) {
+LoadSpec residual_spec(const sepvad_model* h, const Workspace& w, int i, const float* O, const float* R, int Tp) {
   LoadSpec ld{};
   ld.X = O; ld.X2 = R;
-  if (h->cfg.tf_attention) { ld.at = h->ws.at; ld.af = h->ws.af; }
+  if (h->cfg.tf_attention) { ld.at = w.at; ld.af = w.af; }
   const BlockOff& bo = h->blk[i];
   if (h->cfg.ln_mode == SEPVAD_LN_RECURSIVE) {
     ld.mode = LD_RECURSIVE;
-    ld.gn = gn_src(h->ws.rec_mom, Tp / STAT_ROWS, NMOM, 0, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
+    ld.gn = gn_src(w.rec_mom, Tp / STAT_ROWS, NMOM, 0, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
     ld.g2 = h->P(bo.lnb_g); ld.be2 = h->P(bo.lnb_b); ld.eps2 = 1e-5f;
     for (int j = 0; j < 5; ++j) ld.wsum[j] = bo.wsum[j];
   } else if (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL) {
     ld.mode = LD_RESIDUAL;  // (Σr', Σr'²) at offsets 2, 3 of the moment record
-    ld.gn = gn_src(h->ws.rec_mom, Tp / STAT_ROWS, NMOM, 2, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
+    ld.gn = gn_src(w.rec_mom, Tp / STAT_ROWS, NMOM, 2, h->P(bo.lna_g), h->P(bo.lna_b), 1e-5f);
   } else {
     ld.mode = LD_ADD;
   }
@@ -464,12 +491,23 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     h->gate = pk.add(gw);
   }
 #undef BAIL
+  h->split = 1;
+  if (const char* sp = getenv("SEPVAD_SPLIT")) h->split = std::max(1, std::min(MAX_SPLIT, atoi(sp)));
+  bool streams_ok = hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; k < MAX_SPLIT && streams_ok; ++k)
+    streams_ok = hipStreamCreateWithFlags(&h->sub[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&h->join[k], hipEventDisableTiming) == hipSuccess;
+  if (!streams_ok) {
+    g_err = "creating the internal streams/events failed";
+    sepvad_destroy(h);
+    return nullptr;
+  }
   if (hipMalloc(&h->dparams, pk.blob.size() * sizeof(float)) != hipSuccess ||
       hipMemcpy(h->dparams, pk.blob.data(), pk.blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
       hipMalloc(&h->dhalf, pk.hblob.size() * sizeof(__half)) != hipSuccess ||
       hipMemcpy(h->dhalf, pk.hblob.data(), pk.hblob.size() * sizeof(__half), hipMemcpyHostToDevice) != hipSuccess) {
     g_err = "device allocation/upload of the packed weights failed";
-    delete h;
+    sepvad_destroy(h);
     return nullptr;
   }
   return h;
@@ -503,42 +541,33 @@ int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, 
   return SEPVAD_OK;
 }
 
-int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, const SepVadOutputs* out,
-                       const SepVadInferKw* kw, void* stream) {
-  if (!h || !x || !out || !out->sep) return fail(SEPVAD_E_ARG, "sepvad_forward: null argument");
-  if (B < 1) return fail(SEPVAD_E_SHAPE, "sepvad_forward: B must be >= 1");
-  if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
+}  // extern "C"
+
+namespace {
+
+// Per-forward timing state (sepvad_set_timing): HIP events around the GEMM launches of chunk 0.
+struct TimingRec {
+  std::vector<int> gemm_ev, g2_ev;
+};
+
+// Enqueues the forward of utterances [b0, b0 + B) on stream s (model/model.py:402-461).
+int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N, const SepVadOutputs* out,
+                  const SepVadInferKw* kw, hipStream_t s, TimingRec* tr) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
-  DeviceGuard dg(h->device);
-  int rc = ws_reserve(h, B, N);
-  if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
   const SepVadConfig& c = h->cfg;
-  Workspace& w = h->ws;
+  const Workspace w = ws_view(h->ws, b0, Tp);
   const int ntu = Tp / TILE;
-  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-  h->ev.clear();
-  std::vector<int> gemm_ev, g2_ev;
-  if (ev_record(h, s)) return SEPVAD_E_HIP;
+  x += (size_t)b0 * ldx;
+  const size_t u2 = (size_t)b0 * 2;
+  auto ev = [&]() -> int { return tr ? ev_record(h, s) : 0; };
   const size_t g1_grid = (size_t)B * ntu * (CH / TILE);
-  if (const char* pb = getenv("SEPVAD_PROBE_BLOCK")) {
-    h->probe_blk = atoi(pb);
-    const size_t need = 2 * g1_grid * PROBE_SLOTS;
-    if (need > h->probe_n) {
-      if (h->probe) (void)hipFree(h->probe);
-      h->probe = nullptr;
-      h->probe_n = 0;
-      HIPCHK(hipMalloc(&h->probe, need * sizeof(unsigned long long)));
-      h->probe_n = need;
-    }
-    HIPCHK(hipMemsetAsync(h->probe, 0, need * sizeof(unsigned long long), s));
-  }
+  const bool probing = tr && h->probe && h->probe_blk >= 0;
 
   // 1. STFT (spec_input for the spectrum, spec_output for est; identical windows -> one pass)
   {
     StftArgs sa{};
-    sa.B = B; sa.N = N; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
+    sa.B = B; sa.N = N; sa.ldx = ldx; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
     sa.window = h->P(h->win_out);
     sa.X = w.X;
     sa.specdb = h->same_stft_window ? w.specdb : nullptr;
@@ -554,7 +583,8 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
   {
     GateArgs ga{};
     ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
-    ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = w.S0; ga.spec_side = out->spectrum;
+    ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = w.S0;
+    ga.spec_side = out->spectrum ? out->spectrum + (size_t)b0 * NBIN * T : nullptr;
     ga.out_rec = w.rec_gate;
     HIPCHK(launch_gate(ga, s));
   }
@@ -571,16 +601,16 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
       g.ld.mode = LD_GN; g.ld.X = w.S0;   // TCN.LN (model/model.py:333)
       g.ld.gn = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
     } else {
-      g.ld = residual_spec(h, i - 1, w.O[cur], w.R, Tp);
+      g.ld = residual_spec(h, w, i - 1, w.O[cur], w.R, Tp);
     }
     g.Xmat = w.O[nxt];
     g.Y = w.A;
     g.out_rec = w.rec_g1;
-    if (i == h->probe_blk && h->probe) g.probe = h->probe;
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    if (probing && i == h->probe_blk) g.probe = h->probe;
+    if (ev()) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
-    gemm_ev.push_back((int)h->ev.size() - 2);
+    if (ev()) return SEPVAD_E_HIP;
+    if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
     cur = nxt;
 
     DwStatsArgs d{};
@@ -603,12 +633,14 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, 1e-8f);
     g2.foldK = HID; g2.foldc = h->P(bo.fc2);
     g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
-    if (i == h->probe_blk && h->probe) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    if (probing && i == h->probe_blk) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
+    if (ev()) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
-    gemm_ev.push_back((int)h->ev.size() - 2);
-    g2_ev.push_back((int)h->ev.size() - 2);
+    if (ev()) return SEPVAD_E_HIP;
+    if (tr) {
+      tr->gemm_ev.push_back((int)h->ev.size() - 2);
+      tr->g2_ev.push_back((int)h->ev.size() - 2);
+    }
 
     AttStatsArgs at{};
     at.B = B; at.T = T; at.Tp = Tp; at.mtiles = CH / TILE; at.ntiles = ntu; at.tf_att = c.tf_attention;
@@ -622,7 +654,7 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
   {
     HeadStatsArgs hs{};
     hs.B = B; hs.T = T; hs.Tp = Tp;
-    hs.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
+    hs.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
     hs.ld.alpha_h = h->out_a;
     hs.out_rec = w.rec_hs;
     HIPCHK(launch_head_stats(hs, s));
@@ -630,14 +662,14 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
     g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
     set_weights(h, g, h->wout);
     g.bias = h->P(h->bo);
-    g.ld = residual_spec(h, h->nblk - 1, w.O[cur], w.R, Tp);
+    g.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
     g.ld.head = 1; g.ld.alpha_h = h->out_a;
     g.ld.gh = gn_src(w.rec_hs, Tp / STAT_ROWS, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
-    g.Y = w.masks; g.Yside = out->masks_b;
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    g.Y = w.masks; g.Yside = out->masks_b ? out->masks_b + (size_t)b0 * MOUT * T : nullptr;
+    if (ev()) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
-    if (ev_record(h, s)) return SEPVAD_E_HIP;
-    gemm_ev.push_back((int)h->ev.size() - 2);
+    if (ev()) return SEPVAD_E_HIP;
+    if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
   }
   // 5. VAD conv1_1 (model/model.py:424-427,434-436)
   const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
@@ -664,24 +696,72 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
       is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
       is.vy = w.vy; is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
       is.vgn = gn_src(w.rec_vad, Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
-      is.vad_out = out->vad ? out->vad : w.vad;
+      is.vad_out = out->vad ? out->vad + u2 * T : w.vad;
     }
-    is.est_out = (float2*)out->est; is.mask_out = out->mask; is.y = out->sep;
+    is.est_out = out->est ? (float2*)out->est + u2 * NBIN * T : nullptr;
+    is.mask_out = out->mask ? out->mask + u2 * NBIN * T : nullptr;
+    is.y = out->sep + u2 * N;
     HIPCHK(launch_istft(is, s));
   }
-  if (ev_record(h, s)) return SEPVAD_E_HIP;
+  return SEPVAD_OK;
+}
+
+int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const SepVadOutputs* out,
+                 const SepVadInferKw* kw, hipStream_t s) {
+  const int T = 1 + N / HOP;
+  const int Tp = round_up(T, TILE);
+  int rc = ws_reserve(h, B, N);
+  if (rc) return rc;
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+  h->ev.clear();
+  // diagnostics probe (single chunk only)
+  h->probe_blk = -1;
+  if (const char* pb = getenv("SEPVAD_PROBE_BLOCK")) {
+    const size_t need = 2 * (size_t)B * (Tp / TILE) * (CH / TILE) * PROBE_SLOTS;
+    if (need > h->probe_n) {
+      if (h->probe) (void)hipFree(h->probe);
+      h->probe = nullptr;
+      h->probe_n = 0;
+      HIPCHK(hipMalloc(&h->probe, need * sizeof(unsigned long long)));
+      h->probe_n = need;
+    }
+    HIPCHK(hipMemsetAsync(h->probe, 0, need * sizeof(unsigned long long), s));
+    h->probe_blk = atoi(pb);
+  }
+  const int nsplit = (h->probe_blk >= 0 || h->timing) ? 1 : std::max(1, std::min(h->split, B));
+  TimingRec tr;
+  if (nsplit == 1) {
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+    rc = enqueue_chunk(h, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr);
+    if (rc) return rc;
+    if (ev_record(h, s)) return SEPVAD_E_HIP;
+  } else {
+    // fork: every internal stream waits for the caller's stream; join: the caller waits for all
+    HIPCHK(hipEventRecord(h->fork, s));
+    int b0 = 0;
+    for (int k = 0; k < nsplit; ++k) {
+      const int bc = B / nsplit + (k < B % nsplit ? 1 : 0);
+      HIPCHK(hipStreamWaitEvent(h->sub[k], h->fork, 0));
+      rc = enqueue_chunk(h, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr);
+      if (rc) return rc;
+      HIPCHK(hipEventRecord(h->join[k], h->sub[k]));
+      HIPCHK(hipStreamWaitEvent(s, h->join[k], 0));
+      b0 += bc;
+    }
+  }
   if (h->timing) {
     HIPCHK(hipEventSynchronize(h->ev.back()));
     h->gemm_ms = h->g2_ms = 0.0;
-    for (int k : gemm_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->gemm_ms += ms; }
-    for (int k : g2_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->g2_ms += ms; }
+    for (int k : tr.gemm_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->gemm_ms += ms; }
+    for (int k : tr.g2_ev) { float ms; HIPCHK(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1])); h->g2_ms += ms; }
     float tot; HIPCHK(hipEventElapsedTime(&tot, h->ev.front(), h->ev.back()));
     h->total_ms = tot;
-    h->gemm_launches = (int)gemm_ev.size();
-    h->g2_launches = (int)g2_ev.size();
+    h->gemm_launches = (int)tr.gemm_ev.size();
+    h->g2_launches = (int)tr.g2_ev.size();
   }
   if (h->probe && h->probe_blk >= 0) {
     const char* path = getenv("SEPVAD_PROBE_OUT");
+    const size_t g1_grid = (size_t)B * (Tp / TILE) * (CH / TILE);
     std::vector<unsigned long long> hp(2 * g1_grid * PROBE_SLOTS);
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipMemcpy(hp.data(), h->probe, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -697,12 +777,36 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, co
   return SEPVAD_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N, const SepVadOutputs* out,
+                       const SepVadInferKw* kw, void* stream) {
+  return sepvad_forward_strided(h, x, N, B, N, out, kw, stream);
+}
+
+int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int32_t B, int32_t N,
+                               const SepVadOutputs* out, const SepVadInferKw* kw, void* stream) {
+  if (!h || !x || !out || !out->sep) return fail(SEPVAD_E_ARG, "sepvad_forward: null argument");
+  if (B < 1) return fail(SEPVAD_E_SHAPE, "sepvad_forward: B must be >= 1");
+  if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
+  if (ldx < N || ldx > INT32_MAX) return fail(SEPVAD_E_SHAPE, "sepvad_forward: row stride must be >= N");
+  DeviceGuard dg(h->device);
+  return forward_impl(h, x, (int)ldx, B, N, out, kw, (hipStream_t)stream);
+}
+
+int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit) {
+  if (!h || nsplit < 1 || nsplit > MAX_SPLIT) return fail(SEPVAD_E_ARG, "sepvad_set_split: 1 <= n <= 4");
+  h->split = nsplit;
+  return SEPVAD_OK;
+}
 int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {
   if (!h || !x || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_stft: bad arguments");
   DeviceGuard dg(h->device);
   const int T = 1 + N / HOP;
   StftArgs sa{};
-  sa.B = B; sa.N = N; sa.T = T; sa.Tp = round_up(T, TILE); sa.x = x;
+  sa.B = B; sa.N = N; sa.ldx = N; sa.T = T; sa.Tp = round_up(T, TILE); sa.x = x;
   sa.window = h->P(h->win_out); sa.tw = (const float2*)h->P(h->tw);
   sa.Xout = (float2*)X; sa.spec_out = h->same_stft_window ? spec : nullptr;
   HIPCHK(launch_stft(sa, (hipStream_t)stream));
@@ -729,6 +833,11 @@ void sepvad_destroy(sepvad_handle h) {
   DeviceGuard dg(h->device);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   if (h->probe) (void)hipFree(h->probe);
+  for (int k = 0; k < MAX_SPLIT; ++k) {
+    if (h->sub[k]) (void)hipStreamDestroy(h->sub[k]);
+    if (h->join[k]) (void)hipEventDestroy(h->join[k]);
+  }
+  if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->ws.base) (void)hipFree(h->ws.base);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);

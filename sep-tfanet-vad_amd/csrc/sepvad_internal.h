@@ -134,8 +134,8 @@ struct GateArgs {
 constexpr int GATE_ROWS = 16;
 
 struct StftArgs {
-  int B, N, T, Tp;
-  const float* x;        // [B][N]
+  int B, N, ldx, T, Tp;
+  const float* x;        // [B][ldx] (row stride ldx >= N: streaming windows are strided views)
   const float* window;   // [512]
   const float2* tw;      // [512] e^{-2 pi i m / 512}
   float2* X;             // nullable [B][Tp][NBIN]

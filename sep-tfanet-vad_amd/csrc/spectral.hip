@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x, f0 = blockIdx.y * FR_PER_WG;
   for (int i = tid; i < 512; i += 256) tw[i] = a.tw[i];
-  const float* xb = a.x + (size_t)b * a.N;
+  const float* xb = a.x + (size_t)b * a.ldx;
   const int N = a.N;
   for (int round = 0; round < FR_PER_WG / 4; ++round) {
     const int f = f0 + round * 4 + wave;

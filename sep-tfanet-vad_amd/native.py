@@ -19,7 +19,8 @@ SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3 = 0, 1
 PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3}
 
 EXPORTED_SYMBOLS = (
-    "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_stft", "sepvad_istft",
+    "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
+    "sepvad_set_split", "sepvad_stft", "sepvad_istft",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
 
@@ -64,6 +65,11 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_set_precision.argtypes = [P, i32]
     lib.sepvad_forward.restype = i32
     lib.sepvad_forward.argtypes = [P, P, i32, i32, ctypes.POINTER(SepVadOutputs), ctypes.POINTER(SepVadInferKw), P]
+    lib.sepvad_forward_strided.restype = i32
+    lib.sepvad_forward_strided.argtypes = [P, P, ctypes.c_int64, i32, i32, ctypes.POINTER(SepVadOutputs),
+                                           ctypes.POINTER(SepVadInferKw), P]
+    lib.sepvad_set_split.restype = i32
+    lib.sepvad_set_split.argtypes = [P, i32]
     lib.sepvad_stft.restype = i32
     lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft.restype = i32
@@ -164,6 +170,10 @@ class Handle:
         _check(self._lib.sepvad_set_precision(self._h, PRECISIONS[precision]), "sepvad_set_precision")
         self.precision = precision
 
+    def set_split(self, nsplit: int):
+        """Concurrent utterance chunks per forward (1..4; bitwise-identical results)."""
+        _check(self._lib.sepvad_set_split(self._h, int(nsplit)), "sepvad_set_split")
+
     def set_timing(self, on: bool):
         _check(self._lib.sepvad_set_timing(self._h, int(on)), "sepvad_set_timing")
 
@@ -181,8 +191,11 @@ class Handle:
         """One forward. Returns dict(sep, vad, est[, spectrum, masks_b, mask_per_speaker])."""
         if x.device.type != "cuda":
             raise RuntimeError("sepvad forward: input must be a ROCm device tensor")
-        x = x.to(self.device, torch.float32).contiguous()
+        x = x.to(self.device, torch.float32)
+        if x.stride(-1) != 1 or x.stride(0) < x.shape[-1]:
+            x = x.contiguous()
         B, N = x.shape
+        ldx = x.stride(0) if B > 1 else N  # strided row views (streaming windows) need no copy
         T = 1 + N // (self.cfg["n_fftBins"] // 2)
         F = self.cfg["n_fftBins"] // 2 + 1
         S = self.cfg["num_spk"]
@@ -201,8 +214,8 @@ class Handle:
         outs = SepVadOutputs(_ptr(sep).value, _ptr(vad).value, _ptr(est).value, _ptr(spectrum).value,
                              _ptr(masks_b).value, _ptr(mask).value)
         kw = make_kw(inference_kw)
-        rc = self._lib.sepvad_forward(self._h, _ptr(x), B, N, ctypes.byref(outs),
-                                      ctypes.byref(kw) if kw is not None else None, self._stream())
+        rc = self._lib.sepvad_forward_strided(self._h, _ptr(x), ldx, B, N, ctypes.byref(outs),
+                                              ctypes.byref(kw) if kw is not None else None, self._stream())
         _check(rc, "sepvad_forward")
         if vad is None:
             vad_ret = 0  # model/model.py:427
