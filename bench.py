@@ -82,6 +82,79 @@ def cpu_baseline(seconds: float = 12.0):
                        f"in {el:.1f} s, oracle/torch_ref.py fp32 on {threads} threads")
 
 
+def bench_stream(args):
+    """BASELINE cfg 3: OnlineSaving (model/online_class_unknown_targets.py:72-105) over 256 streams of
+    4 s @ 16 kHz, 3 s windows at a 160 ms hop (7 windows per stream, each a batched B=256 forward of
+    48 000 samples, T=188), PIT-L1 realignment and stitching on the device. One step = one calc_online
+    over all streams. value = stream-windows/s (whole job); audio_seconds_per_second = value * save_sec
+    (seconds of new audio emitted per wall-clock second, all streams together)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    import contextlib
+    import io
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    cfg = pkg.CONFIG_WITH_VAD
+    with contextlib.redirect_stdout(io.StringIO()):
+        net = pkg.SeparationModel(**cfg)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_state_dict(cfg, 1234).items()}, strict=True)
+    net = net.eval().to(dev)
+    n_streams, n_total, save_sec = 256, 64000, 0.16
+    x = torch.from_numpy(synth.make_batch(n_streams, n_total, 20_000 + rank * n_streams)[0]).to(dev)
+    net.native_handle(dev).reserve(n_streams, 48000)
+    crit = pkg.PITLossWrapper(loss_func=torch.nn.L1Loss(), pit_from="pw_pt")
+    ons = pkg.OnlineSaving(net, "/nonexistent", crit)
+    ons.save_sec = save_sec
+    n_win = ons.n_windows(n_total)
+    ikw = dict(pkg.INFERENCE_KW_DEFAULTS)
+
+    def step():
+        ons.calc_online(x, "bench", 10 ** 6, ikw)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        windows = world * n_streams * n_win * args.steps
+        out = {
+            "metric": "stream-windows/sec (cfg 3: OnlineSaving, 3 s windows, 160 ms hop, PIT-L1 stitching)",
+            "value": round(windows / el, 2), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic PCG64 mixtures",
+            "config": {"workload": f"cfg3 {n_streams} streams/GPU x {n_total} samples, {n_win} windows of 48000 "
+                                   f"per stream, batched B={n_streams} per window step",
+                       "global_batch": world * n_streams, "seq_len": 48000,
+                       "parallelism": f"dp{world} (independent streams)"},
+            "audio_seconds_per_second": round(windows / el * save_sec, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,7 +168,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="GEMM arithmetic (both meet the fp32 parity gates; see DESIGN.md)")
+    ap.add_argument("--workload", default="offline", choices=["offline", "stream"],
+                    help="offline: cfg 2 (default, the BASELINE metric); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
+    if args.workload == "stream":
+        return bench_stream(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -121,6 +121,25 @@ int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void*
 /* torch.istft(center=True, length=N) of est [B*S, n_fft/2+1, T] complex64 (model/model.py:460). */
 int32_t sepvad_istft(sepvad_handle h, const void* est, int32_t BS, int32_t N, float* y, void* stream);
 
+/* ---- streaming wrapper (model/online_class_unknown_targets.py:72-105) -------------------------
+ * Signals are [B, 2, ld] f32 device arrays (speaker rows of stride ld).
+ *
+ * Replaces PITLossWrapper(nn.L1Loss(), pit_from="pw_pt")(est, ref, return_incides=True)
+ * (model/pit_wrapper.py:77-140,149-177,261-312) on est[..., 0:L] vs ref[..., 0:L]: pairwise L1
+ * means over batch and samples (nn.L1Loss reduces the batch too, so the permutation is shared by
+ * the whole batch), loss set over the 2 permutations, first minimum. Writes perm_out [B, 2] int64
+ * (batch_indices), loss_out (min loss) and pw_out [2, 2] (pairwise losses), each nullable.
+ * scratch: device buffer of at least SEPVAD_PIT_SCRATCH_BYTES. Deterministic. */
+#define SEPVAD_PIT_SCRATCH_BYTES 16384
+int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_t ref_ld, int32_t B, int64_t L,
+                      void* scratch, int64_t* perm_out, float* loss_out, float* pw_out, void* stream);
+
+/* Replaces reorder_source_mse(preds, batch_indices) (model/combined_loss.py:63-78) fused with
+ * OnlineSaving.update_online_signal (online_class_unknown_targets.py:28-37):
+ * dst[b, i, d0 + n] = src[b, perm[b, i], s0 + n] for n < H (perm NULL = identity). */
+int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32_t B, int64_t H,
+                             const int64_t* perm, float* dst, int64_t dst_ld, int64_t d0, void* stream);
+
 /* Seconds of the last forward's dominant-kernel launches measured with HIP events
  * (enabled by sepvad_set_timing(h, 1)); see bench.py. */
 int32_t sepvad_set_timing(sepvad_handle h, int32_t on);

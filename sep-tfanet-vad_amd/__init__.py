@@ -8,8 +8,10 @@ side attributes; the arithmetic runs in hand-written gfx950 HIP kernels behind t
 from .config import (CONFIG_WITH_VAD, CONFIG_WITHOUT_VAD, DEFAULTS, INFERENCE_KW_DEFAULTS,
                      frames, param_spec)
 from .model import SeparationModel
+from .online import OnlineSaving
+from .pit import PITLossWrapper, reorder_source_mse
 
 __all__ = [
-    "SeparationModel", "CONFIG_WITH_VAD", "CONFIG_WITHOUT_VAD", "DEFAULTS",
+    "SeparationModel", "OnlineSaving", "PITLossWrapper", "reorder_source_mse", "CONFIG_WITH_VAD", "CONFIG_WITHOUT_VAD", "DEFAULTS",
     "INFERENCE_KW_DEFAULTS", "param_spec", "frames",
 ]

@@ -828,6 +828,31 @@ int32_t sepvad_istft(sepvad_handle h, const void* est, int32_t BS, int32_t N, fl
   return SEPVAD_OK;
 }
 
+int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_t ref_ld, int32_t B, int64_t L,
+                      void* scratch, int64_t* perm_out, float* loss_out, float* pw_out, void* stream) {
+  if (!est || !ref || !scratch || B < 1 || L < 1 || est_ld < L || ref_ld < L)
+    return fail(SEPVAD_E_ARG, "sepvad_pit_l1: bad arguments");
+  PitArgs a{};
+  a.B = B; a.L = L; a.est = est; a.est_ld = est_ld; a.ref = ref; a.ref_ld = ref_ld;
+  a.nblk = (int)std::min<long long>(PIT_MAX_BLOCKS, std::max<long long>(1, ((long long)B * L + 8191) / 8192));
+  static_assert(PIT_MAX_BLOCKS * 4 * sizeof(double) <= SEPVAD_PIT_SCRATCH_BYTES, "scratch size");
+  a.partial = (double*)scratch;
+  a.perm_out = (long long*)perm_out; a.loss_out = loss_out; a.pw_out = pw_out;
+  HIPCHK(launch_pit_l1(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32_t B, int64_t H,
+                             const int64_t* perm, float* dst, int64_t dst_ld, int64_t d0, void* stream) {
+  if (!src || !dst || B < 1 || H < 1 || s0 < 0 || d0 < 0 || s0 + H > src_ld || d0 + H > dst_ld)
+    return fail(SEPVAD_E_ARG, "sepvad_stream_append: bad arguments");
+  AppendArgs a{};
+  a.B = B; a.H = H; a.src = src; a.src_ld = src_ld; a.s0 = s0; a.perm = (const long long*)perm;
+  a.dst = dst; a.dst_ld = dst_ld; a.d0 = d0;
+  HIPCHK(launch_stream_append(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
 void sepvad_destroy(sepvad_handle h) {
   if (!h) return;
   DeviceGuard dg(h->device);

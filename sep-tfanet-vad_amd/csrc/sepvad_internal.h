@@ -175,6 +175,28 @@ struct IstftArgs {
   float* y;              // [BS][N]
 };
 
+// streaming wrapper (stream.hip)
+constexpr int PIT_MAX_BLOCKS = 512;
+struct PitArgs {
+  int B, nblk;
+  long long L;                 // compared samples per (utterance, speaker)
+  const float* est; long long est_ld;   // [B][2][est_ld], region starts at est
+  const float* ref; long long ref_ld;   // [B][2][ref_ld]
+  double* partial;             // [nblk][4]
+  long long* perm_out;         // nullable [B][2] (torch.long batch_indices)
+  float* loss_out;             // nullable scalar: min permutation loss
+  float* pw_out;               // nullable [2][2] pairwise losses [est][target]
+};
+struct AppendArgs {
+  int B;
+  long long H;                 // samples per speaker row to move
+  const float* src; long long src_ld, s0;
+  const long long* perm;       // nullable [B][2]
+  float* dst; long long dst_ld, d0;
+};
+hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s);
+hipError_t launch_stream_append(const AppendArgs& a, hipStream_t s);
+
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s);

@@ -1,0 +1,94 @@
+// Streaming-wrapper kernels (reference model/online_class_unknown_targets.py:72-105):
+//   k_pit_l1_partial / k_pit_l1_final  PITLossWrapper(nn.L1Loss(), pit_from="pw_pt") with
+//       return_incides=True (model/pit_wrapper.py:77-140,149-177,261-312): pairwise L1 losses between
+//       the new window's overlap region and the stitched signal's tail. nn.L1Loss() reduces over the
+//       batch AND the samples, so every pairwise loss is one scalar shared by the whole batch and the
+//       chosen permutation is batch-global (exactly as the reference computes it).
+//   k_stream_append  reorder_source_mse (model/combined_loss.py:63-78) fused with
+//       OnlineSaving.update_online_signal (online_class_unknown_targets.py:28-37): the reordered last
+//       hop of every window lands in its slot of the preallocated stitched signal (no torch.cat).
+// Layouts: signals are [B][2][ld] fp32 (speaker rows with stride ld). HBM-bound, no MFMA.
+// Reductions are deterministic: fixed per-block ranges, per-block partials in double, summed in
+// block order by the finalizer.
+#include "device_common.h"
+
+namespace sepvad {
+
+constexpr int PIT_THREADS = 256;
+
+// partial[blk][4] = sums over this block's (b, n) range of |est[b][e][n] - ref[b][t][n]|, (e, t) in
+// {(0,0), (0,1), (1,0), (1,1)} (pw_losses[:, est_idx, target_idx], model/pit_wrapper.py:172-177)
+__global__ __launch_bounds__(PIT_THREADS) void k_pit_l1_partial(PitArgs a) {
+  __shared__ float red[4 * 16];
+  const long long total = (long long)a.B * a.L;
+  const long long per = (total + gridDim.x - 1) / gridDim.x;
+  const long long beg = per * blockIdx.x;
+  const long long end = min(total, beg + per);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // fp32 per thread over a short strided range, then double across the block
+  for (long long i = beg + threadIdx.x; i < end; i += PIT_THREADS) {
+    const long long b = i / a.L, n = i % a.L;
+    const float* e = a.est + (size_t)b * 2 * a.est_ld + n;
+    const float* r = a.ref + (size_t)b * 2 * a.ref_ld + n;
+    const float e0 = e[0], e1 = e[a.est_ld], r0 = r[0], r1 = r[a.ref_ld];
+    acc[0] += fabsf(e0 - r0);
+    acc[1] += fabsf(e0 - r1);
+    acc[2] += fabsf(e1 - r0);
+    acc[3] += fabsf(e1 - r1);
+  }
+  block_reduce_store<4>(acc, red, a.partial + (size_t)blockIdx.x * 4);
+}
+
+// One block: pairwise means, the permutation loss set (einsum over one-hot perms / n_src,
+// model/pit_wrapper.py:289-300), torch.min's first-minimum choice (:308), the indices (:311).
+__global__ __launch_bounds__(64) void k_pit_l1_final(PitArgs a, int nblk) {
+  if (threadIdx.x != 0) return;
+  double pw[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < nblk; ++k)
+    for (int j = 0; j < 4; ++j) pw[j] += a.partial[(size_t)k * 4 + j];
+  const double cnt = (double)a.B * (double)a.L;
+  float m[4];
+  for (int j = 0; j < 4; ++j) m[j] = (float)(pw[j] / cnt);
+  // pwl = pw^T (targets x estimates); perms (0,1), (1,0)
+  const float loss_id = (m[0] + m[3]) / 2.f;    // pwl[0][0] + pwl[1][1]
+  const float loss_sw = (m[2] + m[1]) / 2.f;    // pwl[0][1] + pwl[1][0] = pw[1][0] + pw[0][1]
+  const bool swap = loss_sw < loss_id;          // ties keep the first permutation
+  if (a.loss_out) *a.loss_out = swap ? loss_sw : loss_id;
+  if (a.perm_out) {
+    for (int b = 0; b < a.B; ++b) {
+      a.perm_out[2 * b] = swap ? 1 : 0;
+      a.perm_out[2 * b + 1] = swap ? 0 : 1;
+    }
+  }
+  if (a.pw_out)
+    for (int j = 0; j < 4; ++j) a.pw_out[j] = m[j];
+}
+
+hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s) {
+  if (a.B < 1 || a.L < 1 || a.nblk < 1 || a.nblk > PIT_MAX_BLOCKS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pit_l1_partial, dim3(a.nblk), dim3(PIT_THREADS), 0, s, a);
+  hipLaunchKernelGGL(k_pit_l1_final, dim3(1), dim3(64), 0, s, a, a.nblk);
+  return hipGetLastError();
+}
+
+// dst[b][i][d0 + n] = src[b][perm[b][i]][s0 + n], n < H  (perm null = identity)
+__global__ __launch_bounds__(256) void k_stream_append(AppendArgs a) {
+  const long long total = (long long)a.B * 2 * a.H;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long n = i % a.H, bi = i / a.H;
+    const int b = (int)(bi >> 1), s = (int)(bi & 1);
+    const int ps = a.perm ? (int)a.perm[2 * b + s] : s;
+    a.dst[((size_t)b * 2 + s) * a.dst_ld + a.d0 + n] = a.src[((size_t)b * 2 + ps) * a.src_ld + a.s0 + n];
+  }
+}
+
+hipError_t launch_stream_append(const AppendArgs& a, hipStream_t s) {
+  if (a.B < 1 || a.H < 1) return hipErrorInvalidValue;
+  const long long total = (long long)a.B * 2 * a.H;
+  const long long nb = (total + 255) / 256;
+  const int grid = (int)(nb < 4096 ? nb : 4096);
+  hipLaunchKernelGGL(k_stream_append, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sepvad

@@ -94,3 +94,29 @@ def test_si_sdr_formula():
     target = torch.tensor([3.0, -0.5, 2.0, 7.0])
     preds = torch.tensor([2.5, 0.0, 2.0, 8.0])
     assert abs(float(si_sdr(preds, target, zero_mean=False)) - 18.4030) < 1e-3
+
+
+def test_stream_oracle_matches_reference(state_dicts):
+    """oracle/stream_ref.py (streaming wrapper + PIT-L1) vs the reference's calc_online output."""
+    import os
+    from conftest import GOLDEN
+    from oracle.stream_ref import calc_online
+    g = np.load(os.path.join(GOLDEN, "golden_with_vad_stream.npz"))
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    import sep_tfanet_vad_amd as pkg
+    ikw = dict(pkg.INFERENCE_KW_DEFAULTS)
+    online = calc_online(om, torch.from_numpy(g["x"]), save_sec=float(g["save_sec"]), inference_kw=ikw)
+    assert online.shape == g["online"].shape
+    assert np.abs(online.numpy() - g["online"]).max() <= 2e-6
+
+
+def test_pit_l1_batch_global_choice():
+    """nn.L1Loss() means over the batch too: one permutation for the whole batch (pit_wrapper.py:172-177)."""
+    from oracle.stream_ref import pit_l1_pw_pt
+    g = torch.Generator().manual_seed(3)
+    ref = torch.randn(3, 2, 500, generator=g)
+    est = ref.clone()
+    est[0] = ref[0].flip(0) * 1.0       # utterance 0 prefers the swap, weakly outvoted
+    est[1:] += 0.01 * torch.randn(2, 2, 500, generator=g)
+    _, bi = pit_l1_pw_pt(est, ref)
+    assert bi.tolist() == [[0, 1]] * 3
