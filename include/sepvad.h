@@ -140,6 +140,23 @@ int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_
 int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32_t B, int64_t H,
                              const int64_t* perm, float* dst, int64_t dst_ld, int64_t d0, void* stream);
 
+/* ---- input preprocessing of the reference CLI (only_inference.py:68-83) ---------------------
+ * Windowed-sinc resampling filter of torchaudio.transforms.Resample(orig_freq, new_freq) with its
+ * defaults (sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99), host-side, double precision
+ * rounded to float: taps [phases][ntaps] into `taps` (capacity `cap` floats); info receives
+ * {phases, ntaps, stride, width}. Returns SEPVAD_E_ARG if cap is too small. */
+int32_t sepvad_resample_filter(int32_t orig_freq, int32_t new_freq, float* taps, int32_t cap, int32_t* info);
+
+/* Polyphase FIR on the device: y [ylen] = resample(x [n]) with ylen = ceil(new * n / orig) (reduced
+ * by the gcd) and taps (device) from sepvad_resample_filter. */
+int32_t sepvad_resample(const float* x, int64_t n, const float* taps, const int32_t* info, float* y, int64_t ylen,
+                        void* stream);
+
+/* y = 1.8 * (x - min x) / (max x - min x) - 0.9 over n samples (only_inference.py:81), fp32 in the
+ * reference's numpy operation order (bit-exact). scratch: SEPVAD_NORM_SCRATCH_BYTES device bytes. */
+#define SEPVAD_NORM_SCRATCH_BYTES 8192
+int32_t sepvad_normalize(const float* x, int64_t n, float* y, void* scratch, void* stream);
+
 /* Seconds of the last forward's dominant-kernel launches measured with HIP events
  * (enabled by sepvad_set_timing(h, 1)); see bench.py. */
 int32_t sepvad_set_timing(sepvad_handle h, int32_t on);

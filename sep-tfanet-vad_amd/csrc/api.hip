@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -850,6 +851,54 @@ int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32
   a.B = B; a.H = H; a.src = src; a.src_ld = src_ld; a.s0 = s0; a.perm = (const long long*)perm;
   a.dst = dst; a.dst_ld = dst_ld; a.d0 = d0;
   HIPCHK(launch_stream_append(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_resample_filter(int32_t orig_freq, int32_t new_freq, float* taps, int32_t cap, int32_t* info) {
+  if (orig_freq < 1 || new_freq < 1 || !info) return fail(SEPVAD_E_ARG, "sepvad_resample_filter: bad arguments");
+  // torchaudio.functional.functional._get_sinc_resample_kernel, sinc_interp_hann, width 6, rolloff 0.99
+  const int g = std::gcd(orig_freq, new_freq);
+  const int o = orig_freq / g, nw = new_freq / g;
+  const double lpw = 6.0, base = std::min(o, nw) * 0.99;
+  const int width = (int)std::ceil(lpw * o / base);
+  const int ntaps = 2 * width + o;
+  info[0] = nw; info[1] = ntaps; info[2] = o; info[3] = width;
+  if ((long long)nw * ntaps > (1 << 22)) return fail(SEPVAD_E_ARG, "sepvad_resample_filter: ratio too large");
+  if (!taps) return SEPVAD_OK;  // size query
+  if (cap < nw * ntaps) return fail(SEPVAD_E_ARG, "sepvad_resample_filter: taps capacity too small");
+  for (int j = 0; j < nw; ++j) {
+    for (int i = 0; i < ntaps; ++i) {
+      double t = -(double)j / nw + (double)(i - width) / o;
+      t *= base;
+      t = std::min(lpw, std::max(-lpw, t));
+      const double c = std::cos(t * M_PI / lpw / 2.0);
+      const double win = c * c;
+      t *= M_PI;
+      const double k = (t == 0.0) ? 1.0 : std::sin(t) / t;
+      taps[j * ntaps + i] = (float)(k * win * (base / o));
+    }
+  }
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_resample(const float* x, int64_t n, const float* taps, const int32_t* info, float* y, int64_t ylen,
+                        void* stream) {
+  if (!x || !taps || !info || !y || n < 1 || ylen < 1) return fail(SEPVAD_E_ARG, "sepvad_resample: bad arguments");
+  ResampleArgs a{};
+  a.x = x; a.n = n; a.taps = taps; a.phases = info[0]; a.ntaps = info[1]; a.stride = info[2]; a.width = info[3];
+  a.y = y; a.ylen = ylen;
+  const long long full = (long long)std::ceil((double)a.phases * (double)n / (double)a.stride);
+  if (ylen > full) return fail(SEPVAD_E_ARG, "sepvad_resample: ylen exceeds ceil(new * n / orig)");
+  HIPCHK(launch_resample(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_normalize(const float* x, int64_t n, float* y, void* scratch, void* stream) {
+  if (!x || !y || !scratch || n < 1) return fail(SEPVAD_E_ARG, "sepvad_normalize: bad arguments");
+  static_assert(NORM_MAX_BLOCKS * 2 * sizeof(float) <= SEPVAD_NORM_SCRATCH_BYTES, "scratch size");
+  NormArgs a{};
+  a.x = x; a.n = n; a.y = y; a.part = (float*)scratch;
+  HIPCHK(launch_normalize(a, (hipStream_t)stream));
   return SEPVAD_OK;
 }
 

@@ -197,6 +197,22 @@ struct AppendArgs {
 hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s);
 hipError_t launch_stream_append(const AppendArgs& a, hipStream_t s);
 
+// input preprocessing (prep.hip)
+constexpr int NORM_MAX_BLOCKS = 1024;
+struct ResampleArgs {
+  const float* x; long long n;   // input samples
+  const float* taps;             // [phases][ntaps] device
+  int phases, ntaps, stride, width;
+  float* y; long long ylen;
+};
+struct NormArgs {
+  const float* x; long long n;
+  float* y;
+  float* part;                   // [NORM_MAX_BLOCKS][2] scratch
+};
+hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
+hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
+
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s);

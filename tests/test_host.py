@@ -87,3 +87,15 @@ def test_inference_kw_struct():
     assert k.enabled == 1 and k.filter_signals_by_smo_vad == 1 and abs(k.threshold_activated_vad - 0.3) < 1e-7
     with pytest.raises(KeyError):  # the reference indexes the keys directly
         native.make_kw({"threshold_activated_vad": 0.5})
+
+
+def test_resample_filter_matches_restatement():
+    """Host filter of sepvad_resample_filter vs the float64 restatement of torchaudio's kernel (no GPU)."""
+    import numpy as np
+    from oracle.prep_ref import sinc_kernel
+    from sep_tfanet_vad_amd.inference import resample_filter
+    for o, n in ((8000, 16000), (44100, 16000), (22050, 16000), (48000, 16000), (16000, 8000)):
+        taps, info = resample_filter(o, n)
+        k, width, oo, nn = sinc_kernel(o, n)
+        assert info == (nn, 2 * width + oo, oo, width)
+        assert np.abs(taps - k[:, 0, :].numpy()).max() <= 1e-7
