@@ -53,7 +53,7 @@ def res_out_bytes(B, T):
     return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
 
 
-PMC_FILE = "r01g_pmc_res_out.json"
+PMC_FILE = "r01h_pmc_res_out.json"
 DEFAULT_SPLIT = 1
 
 
