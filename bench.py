@@ -46,6 +46,19 @@ def res_out_flops(B, T):
     return 2 * 256 * 512 * B * T
 
 
+def tcn_flops(B, T, nblk=24):
+    """Algorithmic FLOPs of one fused-TCN launch: the two pointwise GEMMs of every block (SURVEY §8d,
+    F_gemm without the output head): 24 * 2 * (256*256 + 512*256) per frame."""
+    return nblk * 2 * (256 * 256 + 512 * 256) * B * T
+
+
+def tcn_bytes(B, T):
+    """Compulsory HBM bytes of one fused-TCN launch: TCN input read + output written (fp32 [B][Tp][256]),
+    the fp16 hi/lo weights in fragment order (24 blocks x 768 KB) read once."""
+    Tp = (T + 63) // 64 * 64
+    return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * 4
+
+
 def res_out_bytes(B, T):
     """Compulsory bytes of one res_out launch: operand d as fp16 hi+lo planes (B*Tp x 512 x 4 B),
     output r fp32 (B*Tp x 256 x 4 B), fp16 hi/lo weights (256 x 512 x 4 B)."""
@@ -53,7 +66,8 @@ def res_out_bytes(B, T):
     return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
 
 
-PMC_FILE = "r01h_pmc_res_out.json"
+PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
+PMC_FILE_FUSED = "r01i_pmc_tcn.json"      # fused schedule (k_tcn)
 DEFAULT_SPLIT = 1
 
 
@@ -242,31 +256,42 @@ def main():
         gemm_ms += tm["gemm_ms"]; res_ms += tm["res_out_ms"]; tot_ms += tm["total_ms"]
         n_res += tm["res_out_launches"]; n_gemm += tm["gemm_launches"]
     h.set_timing(False)
-    torch.cuda.synchronize()
+    fused = h.fused_status()  # synchronises; raises if a fused hand-off gave up
 
     if rank == 0:
         total_utt = world * B * args.steps
         value = total_utt / el
         res_avg_s = res_ms / n_res / 1e3
-        achieved = res_out_flops(B, T) / res_avg_s / 1e12
-        # peak of the arithmetic actually issued: fp16x3 issues 3 fp16 MFMA products per fp32 product
-        if args.precision == "f16x3":
-            peak, kern = F16_MFMA_PEAK_TFLOPS / 3.0, ("k_gemm<F16X3,LD_DW,EP_BIAS_ATT> (DepthConv1d.res_out 512->256 "
-                                                     "with the depthwise conv fused in the operand loader; fp16x3 "
-                                                     "split on v_mfma_f32_32x32x16_f16: peak = 2.5 PF/s / 3)")
+        if fused:
+            # dominant kernel = the fused persistent TCN (all 24 blocks in one launch)
+            flops_launch, bytes_launch = tcn_flops(B, T), tcn_bytes(B, T)
+            peak = F16_MFMA_PEAK_TFLOPS / 3.0
+            kern = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
+                    "512->256, TF-attention, recursive LN], fp16x3 split on v_mfma_f32_32x32x16_f16: peak = "
+                    "2.5 PF/s / 3)")
+            pmc_name = PMC_FILE_FUSED
         else:
-            peak, kern = FP32_MFMA_PEAK_TFLOPS, ("k_gemm<F32,LD_DW,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, "
-                                                 "v_mfma_f32_32x32x2_f32)")
-        fwd_timed = n_gemm / (2 * 24 + 1)  # 49 GEMM launches per forward
+            flops_launch, bytes_launch = res_out_flops(B, T), res_out_bytes(B, T)
+            pmc_name = PMC_FILE
+            # peak of the arithmetic actually issued: fp16x3 issues 3 fp16 MFMA products per fp32 product
+            if args.precision == "f16x3":
+                peak, kern = F16_MFMA_PEAK_TFLOPS / 3.0, ("k_gemm<F16X3,LD_SPLIT,EP_BIAS_ATT> (DepthConv1d.res_out "
+                                                         "512->256; fp16x3 split on v_mfma_f32_32x32x16_f16: peak "
+                                                         "= 2.5 PF/s / 3)")
+            else:
+                peak, kern = FP32_MFMA_PEAK_TFLOPS, ("k_gemm<F32,LD_PLAIN,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, "
+                                                     "v_mfma_f32_32x32x2_f32)")
+        achieved = flops_launch / res_avg_s / 1e12
+        fwd_timed = n_gemm / (2 if fused else 2 * 24 + 1)  # GEMM-bearing launches per forward
         all_gemm_tflops = gemm_flops_per_utt(T) * B * fwd_timed / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
         # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
         # (tools/gpu_round.sh -> tools/pmc.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
         traffic = traffic_src = None
-        pmc = os.path.join(REPO, "profiles", PMC_FILE)
+        pmc = os.path.join(REPO, "profiles", pmc_name)
         if os.path.exists(pmc) and args.precision == "f16x3" and B == B_PER_GPU and N == N_SAMPLES:
             try:
                 traffic = round(json.load(open(pmc))["hbm_bytes_per_launch"])
-                traffic_src = "profiles/" + PMC_FILE
+                traffic_src = "profiles/" + pmc_name
             except (OSError, ValueError, KeyError):
                 traffic = None
         out = {
@@ -283,6 +308,7 @@ def main():
             "dtype": "fp32",
             "gemm_arithmetic": args.precision,
             "split": args.split,
+            "schedule": "fused" if fused else "multi-kernel",
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
                     "recipe weights (pretrained .pth absent from the reference)",
             "config": {
@@ -302,8 +328,8 @@ def main():
                 "frac": round(achieved / peak, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": res_out_bytes(B, T),
-                "flops_per_launch": res_out_flops(B, T),
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "flops_per_launch": flops_launch,
                 "avg_launch_us": round(res_avg_s * 1e6, 2),
                 "all_gemms_tflops": round(all_gemm_tflops, 3) if all_gemm_tflops else None,
                 "gemm_share_of_forward": round(gemm_ms / tot_ms, 3) if tot_ms > 0 else None,

@@ -113,6 +113,15 @@ int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int
  * every reduction is per utterance). Default 1, or the SEPVAD_SPLIT environment variable. */
 int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit);
 
+/* Select the TCN schedule of later forwards: 1 (default, or env SEPVAD_FUSED) = the whole separator stack
+ * as one persistent launch when the GEMMs are F16X3 and T <= 256 (groups of ceil(T/32) workgroups per
+ * utterance); 0 = one launch per stage (4 per block). Both meet the same parity gates. */
+int32_t sepvad_set_fused(sepvad_handle h, int32_t on);
+/* Synchronises the device and reports the schedule of the last forward and the persistent launch's
+ * health: *used = 1 if it ran fused; returns SEPVAD_OK, or SEPVAD_E_HIP if a group hand-off gave up
+ * (a bounded wait timed out; outputs of that forward are invalid). */
+int32_t sepvad_fused_status(sepvad_handle h, int32_t* used);
+
 /* Front-end / back-end stages alone, for kernel-level parity tests:
  * STFT with DC zeroed (model/model.py:16-25,408-410) -> X [B, n_fft/2+1, T] complex64, and
  * 10 log10(clamp(|X|^2, 1e-10)) (model/model.py:411-412) -> spec [B, n_fft/2+1, T] (nullable). */

@@ -43,6 +43,7 @@ int fail(int code, const std::string& msg) {
 // Packed pointwise-conv weight: fp32 [M][K] and the fp16 split of the row-scaled copy.
 struct PackedW {
   size_t w32 = 0, whi = 0, wlo = 0, scale = 0;
+  size_t fhi = 0, flo = 0;  // fused-TCN copies in MFMA B-fragment order (see pack_pointwise)
 };
 
 struct BlockOff {
@@ -112,6 +113,16 @@ struct sepvad_model {
   int split = 1;
   hipStream_t sub[MAX_SPLIT] = {};
   hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
+  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs run fp16x3 and T <= 256
+  bool fused = true;
+  int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU)
+  __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered weights
+  float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
+  float* tpay = nullptr;        // hand-off payload slots [tcn_cap][2][FPAY]
+  unsigned* tflags = nullptr;   // [tcn_cap][2] flags + err word, zeroed before every launch
+  size_t tflag_bytes = 0;
+  bool last_fused = false;
+  unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;
@@ -201,6 +212,23 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   p.scale = pk.add(sc);
   p.whi = pk.addh(hi);
   p.wlo = pk.addh(lo);
+  // k_tcn streams each wave's 32 output rows as consecutive 1 KB fragments (v_mfma_f32_32x32x16_f16
+  // B operand): [mpad/32 row tiles][cin/16 K steps][64 lanes][8 halves], lane l -> row 32*mt + (l & 31),
+  // k = 16*s + 8*(l >> 5) + j.
+  if (mpad % 32 == 0 && cin % 16 == 0) {
+    std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin);
+    size_t q = 0;
+    for (int mt = 0; mt < mpad / 32; ++mt)
+      for (int st = 0; st < cin / 16; ++st)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j, ++q) {
+            const size_t src = (size_t)(32 * mt + (l & 31)) * cin + 16 * st + 8 * (l >> 5) + j;
+            fh[q] = hi[src];
+            fl[q] = lo[src];
+          }
+    p.fhi = pk.addh(fh);
+    p.flo = pk.addh(fl);
+  }
   return p;
 }
 
@@ -291,6 +319,50 @@ LoadSpec residual_spec(const sepvad_model* h, const Workspace& w, int i, const f
     ld.mode = LD_ADD;
   }
   return ld;
+}
+
+// Weight/parameter blobs, hand-off buffers and residency capacity of the fused TCN (fused.hip):
+// per block the fragment-ordered fp16 hi/lo weights (WF_*) and one float parameter blob (PB_*), both
+// contiguous over blocks so the kernel addresses block i with uniform arithmetic (no pointer loads).
+int init_fused(sepvad_model* h, const Packer& pk) {
+  int ncu = 0, dev = h->device;
+  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int ln = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE
+                 : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
+  h->tcn_cap = ncu * tcn_blocks_per_cu(ln);
+  if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
+  std::vector<__half> wf(WF_BLOCK * h->nblk);
+  std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
+  const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
+  for (int i = 0; i < h->nblk; ++i) {
+    const BlockOff& bo = h->blk[i];
+    __half* w = wf.data() + WF_BLOCK * i;
+    std::copy_n(pk.hblob.begin() + bo.w1.fhi, WF_W1L, w);
+    std::copy_n(pk.hblob.begin() + bo.w1.flo, WF_W1L, w + WF_W1L);
+    std::copy_n(pk.hblob.begin() + bo.w2.fhi, WF_W2L - WF_W2H, w + WF_W2H);
+    std::copy_n(pk.hblob.begin() + bo.w2.flo, WF_W2L - WF_W2H, w + WF_W2L);
+    float* q = pb.data() + (size_t)PB_SIZE * i;
+    auto put = [&](int off, size_t src, int n) { std::copy_n(pk.blob.begin() + src, n, q + off); };
+    put(PB_WS1, bo.w1.scale, CH); put(PB_B1, bo.b1, CH); put(PB_G1, bo.g1, CH); put(PB_BE1, bo.be1, CH);
+    put(PB_WD, bo.wd, HID * 3); put(PB_BD, bo.bd, HID);
+    put(PB_WS2, bo.w2.scale, CH); put(PB_B2, bo.b2, CH); put(PB_FC2, bo.fc2, CH);
+    if (rec || res) { put(PB_LNAG, bo.lna_g, CH); put(PB_LNAB, bo.lna_b, CH); }
+    if (rec) { put(PB_LNBG, bo.lnb_g, CH); put(PB_LNBB, bo.lnb_b, CH); }
+    put(PB_ATT, bo.attp, 20);
+    q[PB_A1] = bo.a1; q[PB_A2] = bo.a2;
+    std::memcpy(q + PB_WSUM, bo.wsum, sizeof(bo.wsum));
+    const int li = i % h->cfg.layer;
+    if (bo.dil != (li == 0 ? 1 : (li % 4 + 1))) { g_err = "fused TCN: dilation schedule mismatch"; return SEPVAD_E_ARG; }
+  }
+  HIPCHK(hipMalloc(&h->twf, wf.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->tprm, pb.size() * sizeof(float)));
+  HIPCHK(hipMemcpy(h->tprm, pb.data(), pb.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->tpay, (size_t)h->tcn_cap * 2 * FPAY * sizeof(float)));
+  h->tflag_bytes = ((size_t)h->tcn_cap * 2 + 16) * sizeof(unsigned);  // multiple of 16 bytes
+  HIPCHK(hipMalloc(&h->tflags, h->tflag_bytes));
+  HIPCHK(hipMemset(h->tflags, 0, h->tflag_bytes));
+  return SEPVAD_OK;
 }
 
 }  // namespace
@@ -511,6 +583,11 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     sepvad_destroy(h);
     return nullptr;
   }
+  if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
+  if (init_fused(h, pk) != SEPVAD_OK) {
+    sepvad_destroy(h);
+    return nullptr;
+  }
   return h;
 }
 
@@ -545,6 +622,13 @@ int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, 
 }  // extern "C"
 
 namespace {
+
+// The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 256) and a group fits
+// the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
+bool fused_ok(const sepvad_model* h, int T) {
+  const int G = (T + FR - 1) / FR;
+  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G && h->tflags != nullptr;
+}
 
 // Per-forward timing state (sepvad_set_timing): HIP events around the GEMM launches of chunk 0.
 struct TimingRec {
@@ -589,88 +673,145 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
     ga.out_rec = w.rec_gate;
     HIPCHK(launch_gate(ga, s));
   }
-  // 3. TCN blocks
-  int cur = 0;  // w.O[cur] holds the current block input o once the conv1d GEMM materialized it
-  for (int i = 0; i < h->nblk; ++i) {
-    const BlockOff& bo = h->blk[i];
-    const int nxt = (i == 0) ? 0 : (cur ^ 1);
-    GemmArgs g{};
-    g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH; g.ldy = CH;
-    set_weights(h, g, bo.w1);
-    g.bias = h->P(bo.b1); g.prelu = bo.a1;
-    if (i == 0) {
-      g.ld.mode = LD_GN; g.ld.X = w.S0;   // TCN.LN (model/model.py:333)
-      g.ld.gn = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
-    } else {
-      g.ld = residual_spec(h, w, i - 1, w.O[cur], w.R, Tp);
+  // 3+4. TCN + output head
+  const int G = (T + FR - 1) / FR;
+  const bool use_fused = fused_ok(h, T);
+  h->last_fused = use_fused;
+  if (use_fused) {
+    // one persistent launch for all blocks (fused.hip), then the head GEMM on its output
+    HIPCHK(hipMemsetAsync(h->tflags, 0, h->tflag_bytes, s));
+    TcnArgs ta{};
+    ta.B = B; ta.T = T; ta.Tp = Tp; ta.G = G; ta.nblk = h->nblk; ta.layer = c.layer;
+    ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
+    ta.tf_att = c.tf_attention;
+    ta.wfrag = h->twf; ta.prm = h->tprm; ta.S0 = w.S0;
+    ta.ln = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
+    ta.alpha_h = h->out_a;
+    ta.Xfin = w.O[0]; ta.rec_head = w.rec_hs;
+    ta.pay = h->tpay; ta.flags = h->tflags; ta.err = h->tflags + (size_t)h->tcn_cap * 2;
+    int ngroups = std::min(B, h->tcn_cap / G);
+    if (ngroups >= 8) ngroups -= ngroups % 8;
+    const char* probe_path = getenv("SEPVAD_TCN_PROBE");
+    const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16;
+    if (probe_path) {
+      if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
+      HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
+      ta.probe = h->tprobe;
     }
-    g.Xmat = w.O[nxt];
-    g.Y = w.A;
-    g.out_rec = w.rec_g1;
-    if (probing && i == h->probe_blk) g.probe = h->probe;
     if (ev()) return SEPVAD_E_HIP;
-    HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
+    HIPCHK(launch_tcn(ta, ngroups * G, s));
     if (ev()) return SEPVAD_E_HIP;
-    if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
-    cur = nxt;
-
-    DwStatsArgs d{};
-    d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
-    const GnSrc gn1 = gn_src(w.rec_g1, ntu * (CH / TILE), 2, 0, h->P(bo.g1), h->P(bo.be1), 1e-8f);
-    d.gd1 = gn1; d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
-    d.prec = h->prec; d.Dhi = w.Dhi; d.Dlo = w.Dlo; d.D32 = w.D32;
-    d.out_rec = w.rec_dw;
-    HIPCHK(launch_dw_stats(d, s));
-
-    GemmArgs g2{};
-    g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
-    set_weights(h, g2, bo.w2);
-    g2.bias = h->P(bo.b2);
-    if (h->prec == PREC_F16X3) {
-      g2.ld.mode = LD_SPLIT; g2.ld.Xh = w.Dhi; g2.ld.Xl = w.Dlo;
-    } else {
-      g2.ld.mode = LD_PLAIN; g2.ld.X = w.D32;
+    if (probe_path) {  // diagnostics only: synchronous dump {grid, nblk, G, T} + stamps
+      std::vector<unsigned long long> hp(probe_n);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(hp.data(), h->tprobe, probe_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(probe_path, "wb")) {
+        const long long hdr[4] = {(long long)ngroups * G, h->nblk, G, T};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        fwrite(hp.data(), sizeof(unsigned long long), (size_t)ngroups * G * h->nblk * 16, f);
+        fclose(f);
+      }
     }
-    g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, 1e-8f);
-    g2.foldK = HID; g2.foldc = h->P(bo.fc2);
-    g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
-    if (probing && i == h->probe_blk) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
-    if (ev()) return SEPVAD_E_HIP;
-    HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
-    if (ev()) return SEPVAD_E_HIP;
     if (tr) {
       tr->gemm_ev.push_back((int)h->ev.size() - 2);
       tr->g2_ev.push_back((int)h->ev.size() - 2);
     }
-
-    AttStatsArgs at{};
-    at.B = B; at.T = T; at.Tp = Tp; at.mtiles = CH / TILE; at.ntiles = ntu; at.tf_att = c.tf_attention;
-    at.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
-    at.R = w.R; at.O = w.O[cur]; at.colsum = w.colsum; at.rowsum = w.rowsum; at.attp = h->P(bo.attp);
-    if (c.ln_mode == SEPVAD_LN_RECURSIVE) { at.ga = h->P(bo.lna_g); at.bea = h->P(bo.lna_b); }
-    at.at = w.at; at.af = w.af; at.out_rec = w.rec_mom;
-    HIPCHK(launch_att_stats(at, s));
-  }
-  // 4. output head: PReLU -> GN(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
-  {
-    HeadStatsArgs hs{};
-    hs.B = B; hs.T = T; hs.Tp = Tp;
-    hs.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
-    hs.ld.alpha_h = h->out_a;
-    hs.out_rec = w.rec_hs;
-    HIPCHK(launch_head_stats(hs, s));
     GemmArgs g{};
     g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
     set_weights(h, g, h->wout);
     g.bias = h->P(h->bo);
-    g.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
+    g.ld.mode = LD_PLAIN; g.ld.X = w.O[0];
     g.ld.head = 1; g.ld.alpha_h = h->out_a;
-    g.ld.gh = gn_src(w.rec_hs, Tp / STAT_ROWS, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
+    g.ld.gh = gn_src(w.rec_hs, G, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
     g.Y = w.masks; g.Yside = out->masks_b ? out->masks_b + (size_t)b0 * MOUT * T : nullptr;
     if (ev()) return SEPVAD_E_HIP;
     HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
     if (ev()) return SEPVAD_E_HIP;
     if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
+  } else {
+    // 3. TCN blocks
+    int cur = 0;  // w.O[cur] holds the current block input o once the conv1d GEMM materialized it
+    for (int i = 0; i < h->nblk; ++i) {
+      const BlockOff& bo = h->blk[i];
+      const int nxt = (i == 0) ? 0 : (cur ^ 1);
+      GemmArgs g{};
+      g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH; g.ldy = CH;
+      set_weights(h, g, bo.w1);
+      g.bias = h->P(bo.b1); g.prelu = bo.a1;
+      if (i == 0) {
+        g.ld.mode = LD_GN; g.ld.X = w.S0;   // TCN.LN (model/model.py:333)
+        g.ld.gn = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
+      } else {
+        g.ld = residual_spec(h, w, i - 1, w.O[cur], w.R, Tp);
+      }
+      g.Xmat = w.O[nxt];
+      g.Y = w.A;
+      g.out_rec = w.rec_g1;
+      if (probing && i == h->probe_blk) g.probe = h->probe;
+      if (ev()) return SEPVAD_E_HIP;
+      HIPCHK(launch_gemm(g, EP_PRELU_STATS, s));
+      if (ev()) return SEPVAD_E_HIP;
+      if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
+      cur = nxt;
+
+      DwStatsArgs d{};
+      d.B = B; d.T = T; d.Tp = Tp; d.dil = bo.dil; d.A = w.A;
+      const GnSrc gn1 = gn_src(w.rec_g1, ntu * (CH / TILE), 2, 0, h->P(bo.g1), h->P(bo.be1), 1e-8f);
+      d.gd1 = gn1; d.wd = h->P(bo.wd); d.bd = h->P(bo.bd); d.alpha = bo.a2;
+      d.prec = h->prec; d.Dhi = w.Dhi; d.Dlo = w.Dlo; d.D32 = w.D32;
+      d.out_rec = w.rec_dw;
+      HIPCHK(launch_dw_stats(d, s));
+
+      GemmArgs g2{};
+      g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
+      set_weights(h, g2, bo.w2);
+      g2.bias = h->P(bo.b2);
+      if (h->prec == PREC_F16X3) {
+        g2.ld.mode = LD_SPLIT; g2.ld.Xh = w.Dhi; g2.ld.Xl = w.Dlo;
+      } else {
+        g2.ld.mode = LD_PLAIN; g2.ld.X = w.D32;
+      }
+      g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, 1e-8f);
+      g2.foldK = HID; g2.foldc = h->P(bo.fc2);
+      g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
+      if (probing && i == h->probe_blk) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
+      if (ev()) return SEPVAD_E_HIP;
+      HIPCHK(launch_gemm(g2, EP_BIAS_ATT, s));
+      if (ev()) return SEPVAD_E_HIP;
+      if (tr) {
+        tr->gemm_ev.push_back((int)h->ev.size() - 2);
+        tr->g2_ev.push_back((int)h->ev.size() - 2);
+      }
+
+      AttStatsArgs at{};
+      at.B = B; at.T = T; at.Tp = Tp; at.mtiles = CH / TILE; at.ntiles = ntu; at.tf_att = c.tf_attention;
+      at.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
+      at.R = w.R; at.O = w.O[cur]; at.colsum = w.colsum; at.rowsum = w.rowsum; at.attp = h->P(bo.attp);
+      if (c.ln_mode == SEPVAD_LN_RECURSIVE) { at.ga = h->P(bo.lna_g); at.bea = h->P(bo.lna_b); }
+      at.at = w.at; at.af = w.af; at.out_rec = w.rec_mom;
+      HIPCHK(launch_att_stats(at, s));
+    }
+    // 4. output head: PReLU -> GN(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
+    {
+      HeadStatsArgs hs{};
+      hs.B = B; hs.T = T; hs.Tp = Tp;
+      hs.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
+      hs.ld.alpha_h = h->out_a;
+      hs.out_rec = w.rec_hs;
+      HIPCHK(launch_head_stats(hs, s));
+      GemmArgs g{};
+      g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
+      set_weights(h, g, h->wout);
+      g.bias = h->P(h->bo);
+      g.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
+      g.ld.head = 1; g.ld.alpha_h = h->out_a;
+      g.ld.gh = gn_src(w.rec_hs, Tp / STAT_ROWS, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
+      g.Y = w.masks; g.Yside = out->masks_b ? out->masks_b + (size_t)b0 * MOUT * T : nullptr;
+      if (ev()) return SEPVAD_E_HIP;
+      HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
+      if (ev()) return SEPVAD_E_HIP;
+      if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
+    }
   }
   // 5. VAD conv1_1 (model/model.py:424-427,434-436)
   const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
@@ -729,7 +870,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
     HIPCHK(hipMemsetAsync(h->probe, 0, need * sizeof(unsigned long long), s));
     h->probe_blk = atoi(pb);
   }
-  const int nsplit = (h->probe_blk >= 0 || h->timing) ? 1 : std::max(1, std::min(h->split, B));
+  const int nsplit = (h->probe_blk >= 0 || h->timing || fused_ok(h, T)) ? 1 : std::max(1, std::min(h->split, B));
   TimingRec tr;
   if (nsplit == 1) {
     if (ev_record(h, s)) return SEPVAD_E_HIP;
@@ -802,6 +943,24 @@ int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit) {
   h->split = nsplit;
   return SEPVAD_OK;
 }
+int32_t sepvad_set_fused(sepvad_handle h, int32_t on) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  h->fused = on != 0;
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  DeviceGuard dg(h->device);
+  if (used) *used = h->last_fused ? 1 : 0;
+  if (!h->tflags) return SEPVAD_OK;
+  HIPCHK(hipDeviceSynchronize());
+  unsigned err = 0;
+  HIPCHK(hipMemcpy(&err, h->tflags + (size_t)h->tcn_cap * 2, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up (outputs invalid)");
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {
   if (!h || !x || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_stft: bad arguments");
   DeviceGuard dg(h->device);
@@ -913,6 +1072,11 @@ void sepvad_destroy(sepvad_handle h) {
   }
   if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->ws.base) (void)hipFree(h->ws.base);
+  if (h->twf) (void)hipFree(h->twf);
+  if (h->tprm) (void)hipFree(h->tprm);
+  if (h->tprobe) (void)hipFree(h->tprobe);
+  if (h->tpay) (void)hipFree(h->tpay);
+  if (h->tflags) (void)hipFree(h->tflags);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);
   delete h;

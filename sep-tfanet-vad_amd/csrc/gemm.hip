@@ -396,6 +396,7 @@ static hipError_t dispatch_ld(const GemmArgs& a, dim3 grid, hipStream_t s) {
   if (a.ld.head) {
     if constexpr (EP == EP_BIAS_OUT) {
       switch (lm) {
+        case LD_PLAIN: hipLaunchKernelGGL((k_gemm<PREC, LD_PLAIN, 1, EP>), grid, block, 0, s, a); break;
         case LD_RECURSIVE: hipLaunchKernelGGL((k_gemm<PREC, LD_RECURSIVE, 1, EP>), grid, block, 0, s, a); break;
         case LD_RESIDUAL: hipLaunchKernelGGL((k_gemm<PREC, LD_RESIDUAL, 1, EP>), grid, block, 0, s, a); break;
         case LD_ADD: hipLaunchKernelGGL((k_gemm<PREC, LD_ADD, 1, EP>), grid, block, 0, s, a); break;

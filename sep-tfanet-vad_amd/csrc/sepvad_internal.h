@@ -213,6 +213,38 @@ struct NormArgs {
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
 hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
+// ---- fused persistent TCN (fused.hip) ----
+constexpr int FR = 32;          // frames per workgroup
+constexpr int FG_MAX = 8;       // workgroups per utterance (T <= 256)
+constexpr int FPAY = 2304;      // floats per hand-off payload slot (>= 16 + 8 * 256)
+// Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
+constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine
+constexpr int PB_WD = 1024, PB_BD = 2560;                          // depthwise [512][3], bias [512]
+constexpr int PB_WS2 = 3072, PB_B2 = 3328, PB_FC2 = 3584;          // res_out row scales, folded bias, sum_k W'
+constexpr int PB_LNAG = 3840, PB_LNAB = 4096, PB_LNBG = 4352, PB_LNBB = 4608;  // ln_first / ln_second (or ln_modules)
+constexpr int PB_ATT = 4864;                                       // TF_Attention taps [20] (see AttStatsArgs)
+constexpr int PB_A1 = 4884, PB_A2 = 4885;                          // PReLU slopes
+constexpr int PB_WSUM = 4888;                                      // 5 doubles (8-byte aligned)
+constexpr int PB_SIZE = 4900;                                      // multiple of 4 (float4 staging)
+// fp16 hi/lo weights of one block in MFMA fragment order: conv1d hi | lo (256x256) | res_out hi | lo (256x512)
+constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
+struct TcnArgs {
+  int B, T, Tp, G, nblk, layer, ln_mode, tf_att;
+  const __half* wfrag;   // [nblk][WF_BLOCK] fragment-ordered weights
+  const float* prm;      // [nblk][PB_SIZE] parameter blobs
+  const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
+  GnSrc ln;              // TCN.LN statistics records (k_gate) + affine
+  float alpha_h;         // TCN.output.0 PReLU
+  float* Xfin;           // [B][Tp][CH] TCN output x' (head input)
+  double* rec_head;      // [B][G][2] (sum, sumsq) of PReLU(x') per member
+  float* pay;            // hand-off payload slots [grid][2][FPAY]
+  unsigned* flags;       // [grid][2] (zeroed before every launch)
+  unsigned* err;         // give-up flag (zeroed with the flags)
+  unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
+};
+hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
+int tcn_blocks_per_cu(int ln_mode);
+
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s);

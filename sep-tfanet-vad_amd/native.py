@@ -20,7 +20,7 @@ PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3}
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
-    "sepvad_set_split", "sepvad_stft", "sepvad_istft", "sepvad_pit_l1", "sepvad_stream_append",
+    "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_stft", "sepvad_istft", "sepvad_pit_l1", "sepvad_stream_append",
     "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
@@ -71,6 +71,10 @@ def load_library(path: str = LIB_PATH):
                                            ctypes.POINTER(SepVadInferKw), P]
     lib.sepvad_set_split.restype = i32
     lib.sepvad_set_split.argtypes = [P, i32]
+    lib.sepvad_set_fused.restype = i32
+    lib.sepvad_set_fused.argtypes = [P, i32]
+    lib.sepvad_fused_status.restype = i32
+    lib.sepvad_fused_status.argtypes = [P, ctypes.POINTER(i32)]
     lib.sepvad_stft.restype = i32
     lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft.restype = i32
@@ -185,6 +189,16 @@ class Handle:
     def set_split(self, nsplit: int):
         """Concurrent utterance chunks per forward (1..4; bitwise-identical results)."""
         _check(self._lib.sepvad_set_split(self._h, int(nsplit)), "sepvad_set_split")
+
+    def set_fused(self, on: bool):
+        """TCN schedule of later forwards: one persistent launch (default) or one launch per stage."""
+        _check(self._lib.sepvad_set_fused(self._h, int(bool(on))), "sepvad_set_fused")
+
+    def fused_status(self) -> bool:
+        """Synchronise; True if the last forward ran the fused TCN. Raises if its hand-offs gave up."""
+        used = ctypes.c_int32(0)
+        _check(self._lib.sepvad_fused_status(self._h, ctypes.byref(used)), "sepvad_fused_status")
+        return bool(used.value)
 
     def set_timing(self, on: bool):
         _check(self._lib.sepvad_set_timing(self._h, int(on)), "sepvad_set_timing")

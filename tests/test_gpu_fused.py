@@ -1,0 +1,122 @@
+"""The fused persistent TCN (csrc/fused.hip, one launch for all 24 blocks) against the oracle, the
+reference goldens and the multi-kernel schedule, over every group size it supports (G = ceil(T/32) =
+1..8 workgroups per utterance), batches larger than one resident wave of groups, and the fallback.
+
+Tolerances: separated waveforms max-abs <= 1e-4 vs the reference/oracle (north_star); the two
+schedules differ only in the order of fp32 partial sums, so they agree to 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import CONFIGS, config_of, load_golden
+
+pytestmark = pytest.mark.gpu
+
+SEP_TOL = 1e-4
+SCHED_TOL = 1e-5
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def nets(state_dicts):
+    import sep_tfanet_vad_amd as pkg
+    out = {}
+    for c in CONFIGS:
+        net = pkg.SeparationModel(**config_of(c))
+        net.load_state_dict(state_dicts[c], strict=True)
+        net = net.eval().to(DEV)
+        net.native_precision = "f16x3"
+        out[c] = net
+    return out
+
+
+def _run(net, x, fused, ikw=None):
+    h = net.native_handle(DEV)
+    h.set_fused(fused)
+    with torch.no_grad():
+        sep, vad, est = net(x, ikw) if ikw is not None else net(x)
+    used = h.fused_status()  # synchronises; raises if a hand-off wait gave up
+    h.set_fused(True)
+    return sep, vad, est, used
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+@pytest.mark.parametrize("case", ["small", "ragged", "cfg"])
+def test_fused_matches_reference_goldens(cname, case, nets):
+    g = load_golden(cname, case)
+    sep, vad, _, used = _run(nets[cname], torch.from_numpy(g["x"]).to(DEV), True)
+    assert used, "the fused TCN did not run"
+    sep, vad = sep.cpu().numpy(), vad.cpu().numpy()
+    assert np.abs(sep - g["sep"]).max() <= SEP_TOL
+    assert np.array_equal(vad >= 0.5, g["vad"] >= 0.5)
+    assert np.abs(vad - g["vad"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+@pytest.mark.parametrize("N", [2000, 8000, 12345, 32000, 48000, 64000])
+def test_fused_vs_multikernel_and_oracle(cname, N, nets, state_dicts):
+    """G = 1, 1, 2, 4, 6, 8 workgroups per utterance."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    B = 3
+    x = torch.from_numpy(synth.make_batch(B, N, 31 + N)[0])
+    net = nets[cname]
+    sf, vf, ef, used = _run(net, x.to(DEV), True)
+    assert used
+    sm, vm, em, used_m = _run(net, x.to(DEV), False)
+    assert not used_m
+    assert (sf - sm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= SCHED_TOL
+    assert (ef - em).abs().max().item() <= 1e-3
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    s_ref, v_ref, _ = om(x[:1])
+    assert np.abs(sf[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((vf[:1].cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+
+
+def test_persistent_groups_cover_large_batches(nets):
+    """B above one resident wave of groups (64 groups of 4 at T=126): groups loop over utterances;
+    results are bitwise independent of batch composition and deterministic."""
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    x = torch.from_numpy(synth.make_batch(150, 32000, 4242)[0]).to(DEV)
+    a, va, _, used = _run(net, x, True)
+    assert used
+    b, vb, _, _ = _run(net, x, True)
+    assert torch.equal(a, b) and torch.equal(va, vb)
+    sub = [0, 63, 64, 127, 128, 149]
+    c, vc, _, _ = _run(net, x[sub], True)
+    assert torch.equal(a[sub], c) and torch.equal(va[sub], vc)
+    m, vm, _, _ = _run(net, x[sub], False)
+    assert (c - m).abs().max().item() <= SCHED_TOL
+
+
+def test_inference_kw_on_fused(nets):
+    g = load_golden("with_vad", "small")
+    ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+               threshold_activated_vad=0.5, return_smoothed_vad=True)
+    sep, vad, _, used = _run(nets["with_vad"], torch.from_numpy(g["x"]).to(DEV), True, ikw)
+    assert used
+    assert np.array_equal(vad.cpu().numpy(), g["ikw_vad"])
+    assert np.abs(sep.cpu().numpy() - g["ikw_sep"]).max() <= SEP_TOL
+
+
+def test_long_utterances_fall_back(nets):
+    """T > 256 (N >= 65536) does not fit one group: the multi-kernel schedule runs."""
+    x = torch.rand(1, 70000, device=DEV) * 1.8 - 0.9
+    _, _, _, used = _run(nets["with_vad"], x, True)
+    assert not used
+
+
+def test_fp32_gemms_use_multikernel(nets):
+    net = nets["with_vad"]
+    net.native_precision = "fp32"
+    try:
+        x = torch.rand(2, 8000, device=DEV) * 1.8 - 0.9
+        _, _, _, used = _run(net, x, True)
+        assert not used
+    finally:
+        net.native_precision = "f16x3"

@@ -1,0 +1,30 @@
+"""Phase breakdown of the fused TCN from a SEPVAD_TCN_PROBE dump (wall clock, 100 MHz ticks).
+
+usage: SEPVAD_TCN_PROBE=/tmp/p.bin python bench.py --steps 1 --warmup 1 --no-cpu-baseline
+       python tools/tcn_probe.py /tmp/p.bin
+"""
+import sys
+
+import numpy as np
+
+NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN2 stats", "res_out GEMM",
+         "P2 wait", "rowsum/colsum", "P3 publish+wait", "gates", "moments", "P4 publish+wait", "x' update"]
+
+
+def main(path):
+    raw = np.fromfile(path, dtype=np.int64)
+    grid, nblk, G, T = (int(v) for v in raw[:4])
+    st = raw[4:].astype(np.float64).reshape(grid, nblk, 16)[:, :, :13] / 100.0  # us
+    ok = (st > 0).all(axis=2)
+    d = np.diff(st, axis=2)  # [grid, nblk, 12]
+    print(f"grid={grid} nblk={nblk} G={G} T={T}; workgroups with full stamps: {ok.all(axis=1).sum()}")
+    blk = (st[:, :, 12] - st[:, :, 0])
+    print(f"per block (median over workgroups): {np.median(blk):.2f} us; first block start spread "
+          f"{st[:, 0, 0].max() - st[:, 0, 0].min():.2f} us; launch span {st[:, -1, 12].max() - st[:, 0, 0].min():.1f} us")
+    for i, n in enumerate(NAMES):
+        v = d[:, 1:, i]  # skip block 0 (cold)
+        print(f"  {n:24s} median {np.median(v):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
