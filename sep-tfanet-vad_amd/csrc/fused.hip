@@ -73,8 +73,11 @@ __device__ __forceinline__ Tp* uni(Tp* p) {
 __device__ __forceinline__ float unif(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
 }
+// Buffer descriptor over a wave-uniform base. The base goes through readfirstlane: under SGPR pressure
+// hipcc keeps uniform pointers in VGPRs, and a descriptor it cannot prove uniform turns every buffer
+// access into a waterfall loop (cdna_hip_programming.md T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uni(p)), (short)0, 0x7fffffff, 0x00020000);
 }
 // Write-through (sc1) stores / sc1 loads of hand-off payload, addressed as float offsets from the
 // (wave-uniform) payload base: aux 16 = sc1 on gfx950.
@@ -191,6 +194,47 @@ __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, int idx,
       a.probe[((size_t)blockIdx.x * a.nblk + bi) * 16 + (k)] = wall_clock64();                     \
   } while (0)
 
+// DPP lane reductions (no LDS round trip, fixed order => deterministic). update_dpp with old = 0:
+// lanes whose DPP source is out of range add 0.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// quad_perm [1,0,3,2], [2,3,0,1], row_shr:4, row_shr:8, row_bcast:15 => lane 31 holds the sum of lanes
+// 0..31 and lane 63 the sum of lanes 32..63.
+__device__ __forceinline__ float half_total(float v) {
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  v += dpp_f<0x142>(v);
+  return v;
+}
+// Sum over the 64 lanes (+ row_bcast:31), returned wave-uniform (lane 63).
+__device__ __forceinline__ float wave_total(float v) {
+  v = half_total(v);
+  v += dpp_f<0x143>(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+// Block sums of NV per-thread values (512 threads): waves by DPP, the 8 wave totals in double in wave
+// order by thread j < NV into out[j]. One barrier; callers barrier again before reading `out`.
+template <int NV>
+__device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* out) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float t = wave_total(v[j]);
+    if ((threadIdx.x & 63) == 0) lds[j * 8 + w] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += lds[threadIdx.x * 8 + i];
+    out[threadIdx.x] = t;
+  }
+}
+
 template <int LM>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   __shared__ __attribute__((aligned(16))) TcnSmem sm;
@@ -289,7 +333,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sm.H[(tl + 4) * CH + m] = v;
           st[0] += v; st[1] += v * v;
         }
-        block_reduce_store<2>(st, sm.red, sm.dred);  // barrier inside: H complete
+        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H complete
       TPROBE(2);
       }
       // ---- P1: GN1 partial sums + boundary rows (first dil / last dil own frames) ----
@@ -374,7 +418,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             split_store(sm.Ahi, sm.Alo, tl * LDD + 2 * c + q, v);
           }
         }
-        block_reduce_store<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
+        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
       }
       // ---- P2: GN2 partial sums (awaited after the res_out main loop) ----
@@ -412,7 +456,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
           const bool valid = t0 + tl < T;
           if (valid) rsum += rv[r];
-          if (tf) sm.H[tl * CH + m] = valid ? rv[r] : 0.f;
+          if (tf) {  // this frame's sum over the wave's 32 channels (lane 31: half 0 rows, lane 63: half 1)
+            const float cs = half_total(valid ? rv[r] : 0.f);
+            if ((lane & 31) == 31) sm.cs[tl][wave] = cs;
+          }
         }
         if (tf) {
           rsum += __shfl_xor(rsum, 32);
@@ -421,14 +468,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       // ---- TF_Attention (model/model.py:182-208): P3 = channel sums over own frames + per-frame sums ----
       if (tf) {
-        __syncthreads();
-        if (tid < FR * 8) {  // frame tid/8, channel slice (tid%8)*32 .. +32
-          const int tl = tid >> 3, sl = tid & 7;
-          float s = 0.f;
-#pragma unroll 8
-          for (int j = 0; j < 32; ++j) s += sm.H[tl * CH + sl * 32 + j];
-          sm.cs[tl][sl] = s;
-        }
         __syncthreads();
         if (tid < FR) {
           float s = 0.f;
@@ -508,7 +547,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             mo[2] += rp; mo[3] += rp * rp;
           }
         }
-        block_reduce_store<NMOM>(mo, sm.red, sm.dred);
+        block_sums<NMOM>(mo, sm.red, sm.dred);
       TPROBE(10);
         // ---- P4 ----
         const unsigned e = xc.ep + 1;
@@ -571,7 +610,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           st[0] += pv; st[1] += pv * pv;
         }
       }
-      block_reduce_store<2>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
+      block_sums<2>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
       __syncthreads();
     }
   }
