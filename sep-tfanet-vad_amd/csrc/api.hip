@@ -688,6 +688,7 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
     ta.ln = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
     ta.alpha_h = h->out_a;
     ta.Xfin = w.O[0]; ta.rec_head = w.rec_hs;
+    ta.xmode = getenv("SEPVAD_TCN_XMODE") ? atoi(getenv("SEPVAD_TCN_XMODE")) : 0;
     ta.pay = h->tpay; ta.flags = h->tflags; ta.err = h->tflags + (size_t)h->tcn_cap * 2;
     int ngroups = std::min(B, h->tcn_cap / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;

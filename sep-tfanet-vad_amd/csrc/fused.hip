@@ -84,6 +84,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
 __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int foff, float4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, foff * 4, 0, 16);
 }
+// Same-XCD groups: plain stores keep the line in the shared L2, where the consumers' sc1 loads (L1
+// bypass) find it; the drain before the flag makes the stores complete at L2 first.
+__device__ __forceinline__ void st_l2(__amdgpu_buffer_rsrc_t r, int foff, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, foff * 4, 0, 0);
+}
 __device__ __forceinline__ float4 ld_wt(__amdgpu_buffer_rsrc_t r, int foff) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, foff * 4, 0, 16));
 }
@@ -109,14 +114,23 @@ struct Xchg {
   int base, G, g;            // first member's index, members, own member index
   unsigned ep;               // epochs published so far
   bool failed;               // thread 0: a wait gave up (skip later waits)
+  bool l2;                   // every member on this workgroup's XCD: payload and flags stay in its L2
 
+  __device__ void store(int foff, float4 v) const {
+    if (l2) st_l2(pay, foff, v);
+    else st_wt(pay, foff, v);
+  }
   __device__ int slot(int member, unsigned e) const { return ((base + member) * 2 + (int)(e & 1)) * FPAY; }
   // after wave 0 stored the payload of epoch ep+1 into slot(g, ep+1): drain, flag
   __device__ void publish(int wave, int lane) {
     ++ep;
     if (wave == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(flags + (size_t)(base + g) * 2 + (ep & 1), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned* f = flags + (size_t)(base + g) * 2 + (ep & 1);
+      if (lane == 0) {
+        if (l2) *reinterpret_cast<volatile unsigned*>(f) = ep;
+        else __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   // thread 0 waits for every other member's flag of epoch e; the caller then barriers
@@ -251,8 +265,25 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     g = blockIdx.x % G;
   }
   const int ngroups = gridDim.x / G;
-  Xchg xc{rsrc_of(a.pay), a.flags, a.err, grp * G, G, g, 0u, false};
+  Xchg xc{rsrc_of(a.pay), a.flags, a.err, grp * G, G, g, 0u, false, false};
   const __amdgpu_buffer_rsrc_t pr = xc.pay;
+  // epoch 1: the members' XCD ids (write-through protocol); if the whole group shares one XCD, every later
+  // hand-off keeps its bytes in that XCD's L2 (correct for any placement: checked, not assumed)
+  {
+    const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+    if (tid == 0) st_wt(pr, xc.slot(g, 1), make_float4(__builtin_bit_cast(float, xcc), 0.f, 0.f, 0.f));
+    xc.publish(wave, lane);
+    xc.wait(1);
+    __syncthreads();
+    if (tid == 0) {
+      bool same = a.xmode == 0;
+      for (int mm = 0; mm < G; ++mm) same = same && __builtin_bit_cast(unsigned, ld_wt1(pr, xc.slot(mm, 1))) == xcc;
+      sm.red[0] = same ? 1.f : 0.f;
+    }
+    __syncthreads();
+    xc.l2 = sm.red[0] != 0.f;
+    __syncthreads();
+  }
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const int m = 32 * wave + (lane & 31);            // this lane's output channel in both GEMMs
   const int hl = lane >> 5;
@@ -342,13 +373,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const int dst = xc.slot(g, e);
         __syncthreads();
         if (wave == 0) {
-          if (lane == 0) st_wt(pr, dst + 0, dd_as_f4(sm.dred[0], sm.dred[1]));
+          if (lane == 0) xc.store(dst + 0, dd_as_f4(sm.dred[0], sm.dred[1]));
           // rows 0..dil-1 -> [16, 16 + dil*256); rows 32-dil..31 -> [16 + 4*256, ...)
           for (int i = lane; i < 2 * dil * (CH / 4); i += 64) {
             const int j = i / (CH / 4), c4 = (i % (CH / 4)) * 4;
             const int tl = j < dil ? j : FR - 2 * dil + j;
             const int off = j < dil ? 16 + j * CH : 16 + 4 * CH + (j - dil) * CH;
-            st_wt(pr, dst + off + c4, *reinterpret_cast<const float4*>(&sm.H[(tl + 4) * CH + c4]));
+            xc.store(dst + off + c4, *reinterpret_cast<const float4*>(&sm.H[(tl + 4) * CH + c4]));
           }
         }
         xc.publish(wave, lane);
@@ -425,7 +456,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const unsigned e2 = xc.ep + 1;
       {
         __syncthreads();
-        if (wave == 0 && lane == 0) st_wt(pr, xc.slot(g, e2), dd_as_f4(sm.dred[0], sm.dred[1]));
+        if (wave == 0 && lane == 0) xc.store(xc.slot(g, e2), dd_as_f4(sm.dred[0], sm.dred[1]));
         xc.publish(wave, lane);
       }
       // ================= res_out 512->256 (model/model.py:136,144) with reg2 folded =================
@@ -480,8 +511,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const unsigned e = xc.ep + 1;
         if (wave == 0) {
           const int dst = xc.slot(g, e);
-          st_wt(pr, dst + 4 * lane, *reinterpret_cast<const float4*>(&sm.vec[4 * lane]));     // [0, 256)
-          if (lane < FR / 4) st_wt(pr, dst + CH + 4 * lane, *reinterpret_cast<const float4*>(&sm.mC[4 * lane]));
+          xc.store(dst + 4 * lane, *reinterpret_cast<const float4*>(&sm.vec[4 * lane]));     // [0, 256)
+          if (lane < FR / 4) xc.store(dst + CH + 4 * lane, *reinterpret_cast<const float4*>(&sm.mC[4 * lane]));
         }
         xc.publish(wave, lane);
         xc.wait(e);
@@ -554,7 +585,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         __syncthreads();
         if (wave == 0 && lane < 6) {
           const double d0 = sm.dred[2 * lane], d1 = 2 * lane + 1 < NMOM ? sm.dred[2 * lane + 1] : 0.0;
-          st_wt(pr, xc.slot(g, e) + 4 * lane, dd_as_f4(d0, d1));
+          xc.store(xc.slot(g, e) + 4 * lane, dd_as_f4(d0, d1));
         }
         xc.publish(wave, lane);
         xc.wait(e);

@@ -240,6 +240,8 @@ struct TcnArgs {
   float* pay;            // hand-off payload slots [grid][2][FPAY]
   unsigned* flags;       // [grid][2] (zeroed before every launch)
   unsigned* err;         // give-up flag (zeroed with the flags)
+  int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
+                         // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);

@@ -120,3 +120,20 @@ def test_fp32_gemms_use_multikernel(nets):
         assert not used
     finally:
         net.native_precision = "f16x3"
+
+
+def test_handoff_protocols_bitwise_identical(nets):
+    """Same-XCD groups keep hand-off bytes in L2 (plain stores); SEPVAD_TCN_XMODE=1 forces the
+    write-through protocol everywhere. Only the transport differs, so the bits must not."""
+    import os
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    x = torch.from_numpy(synth.make_batch(70, 32000, 777)[0]).to(DEV)
+    a, va, _, _ = _run(net, x, True)
+    os.environ["SEPVAD_TCN_XMODE"] = "1"
+    try:
+        b, vb, _, used = _run(net, x, True)
+    finally:
+        del os.environ["SEPVAD_TCN_XMODE"]
+    assert used
+    assert torch.equal(a, b) and torch.equal(va, vb)
