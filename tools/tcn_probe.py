@@ -14,7 +14,8 @@ NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN
 def main(path):
     raw = np.fromfile(path, dtype=np.int64)
     grid, nblk, G, T = (int(v) for v in raw[:4])
-    st = raw[4:].astype(np.float64).reshape(grid, nblk, 16)[:, :, :13] / 100.0  # us
+    full = raw[4:].astype(np.float64).reshape(grid, nblk, 16) / 100.0  # us
+    st = full[:, :, :13]
     ok = (st > 0).all(axis=2)
     d = np.diff(st, axis=2)  # [grid, nblk, 12]
     print(f"grid={grid} nblk={nblk} G={G} T={T}; workgroups with full stamps: {ok.all(axis=1).sum()}")
@@ -24,6 +25,10 @@ def main(path):
     for i, n in enumerate(NAMES):
         v = d[:, 1:, i]  # skip block 0 (cold)
         print(f"  {n:24s} median {np.median(v):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+    cyc = full[:, 1:, 14] - full[:, 1:, 13]  # shader clock ticks (x100: the array was scaled to us)
+    if (cyc > 0).all():
+
+        print(f"shader clock during the blocks: {np.median(cyc * 100.0 / blk[:, 1:]) / 1e3:.2f} GHz (s_memtime ticks / wall us)")
 
 
 if __name__ == "__main__":
