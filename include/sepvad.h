@@ -149,6 +149,27 @@ int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_
 int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32_t B, int64_t H,
                              const int64_t* perm, float* dst, int64_t dst_ld, int64_t d0, void* stream);
 
+/* ---- quality metrics (model/combined_loss.py:16-56 calc_sisdr == model/metric.py:61-101
+ * scale_invariant_signal_distortion_ratio; PIT over it: metric.py:258 pit_si_sdr) --------------------
+ * out[r] = SI-SDR(P[pidx[r]], Tg[tidx[r]]) in dB for r < R: rows of N samples with row strides p_ld / t_ld,
+ * pidx / tidx nullable (identity). eps = float32 epsilon; zero_mean as the reference's flag. Moments in
+ * double, fixed-order reductions (bitwise reproducible). Device pointers, stream-ordered. */
+int32_t sepvad_si_sdr(const float* P, int64_t p_ld, const float* Tg, int64_t t_ld, int64_t N, int32_t R,
+                      const int32_t* pidx, const int32_t* tidx, int32_t zero_mean, float* out, void* stream);
+
+/* ---- synthetic reverberant mixtures (BASELINE cfg 4): image-method room impulse responses --------
+ * Replaces pyrirgen.generateRir / gen_rir (create_data/rirgen.cpp:115-351, create_data/pyrirgen.pyx)
+ * as create_data/create_simulation_data.py:284-289 calls it. HOST function, double precision:
+ * c sound speed (m/s), fs (Hz), mics [n_mics][3] and src [3] positions (m), room [3] dimensions (m),
+ * beta: n_beta = 1 -> T60 (s; 0 = anechoic) or n_beta = 6 -> reflection coefficients, orientation [2]
+ * (azimuth, elevation; nullable = 0), high_pass 1/0, n_dim 2/3, order (-1 = all), n_samples (-1 = T60 fs),
+ * mic_type 'o','s','c','h','b'. Writes out [n_mics][n_samples] (cap doubles) and returns n_samples;
+ * out NULL = size query. Negative status on bad arguments. */
+int32_t sepvad_rir_generate(double c, double fs, const double* mics, int32_t n_mics, const double* src,
+                            const double* room, const double* beta, int32_t n_beta, const double* orientation,
+                            int32_t high_pass, int32_t n_dim, int32_t order, int32_t n_samples, char mic_type,
+                            double* out, int64_t cap);
+
 /* ---- input preprocessing of the reference CLI (only_inference.py:68-83) ---------------------
  * Windowed-sinc resampling filter of torchaudio.transforms.Resample(orig_freq, new_freq) with its
  * defaults (sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99), host-side, double precision

@@ -1053,6 +1053,16 @@ int32_t sepvad_resample(const float* x, int64_t n, const float* taps, const int3
   return SEPVAD_OK;
 }
 
+int32_t sepvad_si_sdr(const float* P, int64_t p_ld, const float* Tg, int64_t t_ld, int64_t N, int32_t R,
+                      const int32_t* pidx, const int32_t* tidx, int32_t zero_mean, float* out, void* stream) {
+  if (!P || !Tg || !out || N < 1 || R < 1 || p_ld < N || t_ld < N) return fail(SEPVAD_E_ARG, "sepvad_si_sdr: bad arguments");
+  SiSdrArgs a{};
+  a.P = P; a.p_ld = p_ld; a.Tg = Tg; a.t_ld = t_ld; a.N = N; a.R = R; a.pidx = pidx; a.tidx = tidx;
+  a.zero_mean = zero_mean; a.out = out;
+  HIPCHK(launch_si_sdr(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_normalize(const float* x, int64_t n, float* y, void* scratch, void* stream) {
   if (!x || !y || !scratch || n < 1) return fail(SEPVAD_E_ARG, "sepvad_normalize: bad arguments");
   static_assert(NORM_MAX_BLOCKS * 2 * sizeof(float) <= SEPVAD_NORM_SCRATCH_BYTES, "scratch size");

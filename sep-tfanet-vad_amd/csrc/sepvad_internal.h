@@ -211,6 +211,17 @@ struct NormArgs {
   float* part;                   // [NORM_MAX_BLOCKS][2] scratch
 };
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
+
+// quality metrics (metrics.hip)
+struct SiSdrArgs {
+  const float* P; long long p_ld;
+  const float* Tg; long long t_ld;
+  long long N; int R;
+  const int* pidx; const int* tidx;
+  int zero_mean;
+  float* out;
+};
+hipError_t launch_si_sdr(const SiSdrArgs& a, hipStream_t s);
 hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
 // ---- fused persistent TCN (fused.hip) ----

@@ -21,7 +21,7 @@ PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3}
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_stft", "sepvad_istft", "sepvad_pit_l1", "sepvad_stream_append",
-    "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize",
+    "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_rir_generate",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
 
@@ -90,6 +90,12 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_resample.argtypes = [P, i64, P, P, P, i64, P]
     lib.sepvad_normalize.restype = i32
     lib.sepvad_normalize.argtypes = [P, i64, P, P, P]
+    lib.sepvad_si_sdr.restype = i32
+    lib.sepvad_si_sdr.argtypes = [P, i64, P, i64, i64, i32, P, P, i32, P, P]
+    dptr = ctypes.POINTER(ctypes.c_double)
+    lib.sepvad_rir_generate.restype = i32
+    lib.sepvad_rir_generate.argtypes = [ctypes.c_double, ctypes.c_double, dptr, i32, dptr, dptr, dptr, i32, dptr,
+                                        i32, i32, i32, i32, ctypes.c_char, dptr, i64]
     lib.sepvad_set_timing.restype = i32
     lib.sepvad_set_timing.argtypes = [P, i32]
     lib.sepvad_timing.restype = i32

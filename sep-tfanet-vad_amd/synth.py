@@ -116,3 +116,46 @@ def make_batch(batch: int, n_samples: int, base_seed: int = 2024):
         mixes.append(m)
         srcs.append(s)
     return np.stack(mixes), np.stack(srcs)
+
+
+def make_reverb_mixture(n_samples: int, seed: int, fs: int = FS, rt60=(0.2, 0.6), rir_samples: int | None = None):
+    """BASELINE cfg 4 input: two sources convolved with image-method RIRs of a random shoebox room
+    (RT60 ~ U[rt60], create_data/data_conifg_wham.yaml:54-55; generator: sepvad_rir_generate, the
+    reference's rirgen restated) plus coloured noise at SNR ~ U[0,15] dB (WHAM! noise is not available
+    offline), min-max normalised like only_inference.py:81.
+
+    Returns (mix[N], direct-path sources[2, N]) in float32 (targets: anechoic RIRs, T60 = 0)."""
+    from scipy.signal import fftconvolve
+    from .rirgen import generateRir
+    rng = np.random.Generator(np.random.PCG64(seed))
+    room = rng.uniform([3.0, 3.0, 2.2], [8.0, 7.0, 3.5])
+    mic = rng.uniform(0.2, 0.8, 3) * room
+    t60 = float(rng.uniform(*rt60))
+    n_rir = rir_samples or int(t60 * fs)
+    rev, dry = [], []
+    for _ in range(2):
+        s = _source(rng, n_samples, fs)
+        s /= np.sqrt(np.mean(s ** 2)) + 1e-9
+        pos = rng.uniform(0.15, 0.85, 3) * room
+        h = np.array(generateRir(list(room), list(pos), list(mic), reverbTime=t60, fs=fs, nSamples=n_rir))
+        h0 = np.array(generateRir(list(room), list(pos), list(mic), reverbTime=0.0, fs=fs, nSamples=n_rir))
+        rev.append(fftconvolve(s, h)[:n_samples])
+        dry.append(fftconvolve(s, h0)[:n_samples])
+    speech = rev[0] + rev[1]
+    snr = rng.uniform(0.0, 15.0)
+    noise = _ar1_noise(rng, n_samples, rng.uniform(0.3, 0.9))
+    noise *= np.sqrt(np.mean(speech ** 2) / (np.mean(noise ** 2) * 10 ** (snr / 10)))
+    mix = speech + noise
+    lo, hi = mix.min(), mix.max()
+    scale = 1.8 / (hi - lo)
+    mix_n = scale * (mix - lo) - 0.9
+    return mix_n.astype(np.float32), (scale * np.stack(dry)).astype(np.float32)
+
+
+def make_reverb_batch(batch: int, n_samples: int, base_seed: int = 4096, **kw):
+    """[B, N] reverberant mixtures and [B, 2, N] direct-path sources; utterance b uses PCG64(base_seed + b).
+    RIRs are generated in parallel host threads (the C call releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        res = list(ex.map(lambda b: make_reverb_mixture(n_samples, base_seed + b, **kw), range(batch)))
+    return np.stack([r[0] for r in res]), np.stack([r[1] for r in res])

@@ -1,0 +1,57 @@
+"""BASELINE configs beyond the headline one, as parity cases:
+  cfg 4: 8 s reverberant mixtures (image-method RIRs, RT60 U[0.2, 0.6]) -> T = 251, 8 workgroups per group;
+  cfg 5: GEMM precision sweep (fp32 MFMA vs fp16x3 split) against the fp32 oracle on cfg-2 inputs.
+Both against oracle/torch_ref.py (fp32, CPU) at sizes it finishes in seconds."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import config_of
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SEP_TOL = 1e-4
+
+
+def _net(cname, state_dicts, precision):
+    import sep_tfanet_vad_amd as pkg
+    net = pkg.SeparationModel(**config_of(cname))
+    net.load_state_dict(state_dicts[cname], strict=True)
+    net = net.eval().to(DEV)
+    net.native_precision = precision
+    return net
+
+
+def _check(sep, vad, s_ref, v_ref):
+    err = np.abs(sep - s_ref).max()
+    assert err <= SEP_TOL, f"sep max-abs {err}"
+    safe = np.abs(v_ref - 0.5) > 1e-4
+    assert np.array_equal((vad >= 0.5)[safe], (v_ref >= 0.5)[safe])
+    return err
+
+
+def test_cfg4_reverberant_8s(state_dicts):
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    x, _ = synth.make_reverb_batch(2, 64000, 9100, rir_samples=4000)
+    net = _net("with_vad", state_dicts, "f16x3")
+    with torch.no_grad():
+        sep, vad, _ = net(torch.from_numpy(x).to(DEV))
+    assert net.native_handle(DEV).fused_status()  # T = 251 runs fused (G = 8)
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    s_ref, v_ref, _ = om(torch.from_numpy(x))
+    _check(sep.cpu().numpy(), vad.cpu().numpy(), s_ref.numpy(), v_ref.numpy())
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_cfg5_precision_sweep(precision, state_dicts):
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    x, _ = synth.make_batch(4, 32000, 5150)
+    net = _net("with_vad", state_dicts, precision)
+    with torch.no_grad():
+        sep, vad, _ = net(torch.from_numpy(x).to(DEV))
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    s_ref, v_ref, _ = om(torch.from_numpy(x))
+    err = _check(sep.cpu().numpy(), vad.cpu().numpy(), s_ref.numpy(), v_ref.numpy())
+    print(f"cfg5 {precision}: sep max-abs vs fp32 oracle {err:.2e}")

@@ -120,3 +120,13 @@ def test_pit_l1_batch_global_choice():
     est[1:] += 0.01 * torch.randn(2, 2, 500, generator=g)
     _, bi = pit_l1_pw_pt(est, ref)
     assert bi.tolist() == [[0, 1]] * 3
+
+
+def test_oracle_si_sdr_known_answer():
+    """The oracle's calc_sisdr restatement reproduces the reference docstring example
+    (model/combined_loss.py:31-33): 18.4030 dB. The example is torchmetrics' (zero_mean=False there,
+    the reference's function defaults to True)."""
+    import torch
+    from oracle.torch_ref import si_sdr
+    v = si_sdr(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]), zero_mean=False).item()
+    assert abs(v - 18.4030) < 1e-4
