@@ -100,6 +100,29 @@ __device__ __forceinline__ double ld_wtd(__amdgpu_buffer_rsrc_t r, int foff) {  
   const unsigned hi = __builtin_amdgcn_raw_buffer_load_b32(r, foff * 4 + 4, 0, 16);
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
+// Sum over the group's members (in member order) of the double / float at float offset `off` of each
+// member's slot of epoch e: all loads issued before the first add (one latency, not G).
+template <typename Slot>
+__device__ __forceinline__ double sum_members_d(__amdgpu_buffer_rsrc_t r, const Slot& slot, int G, unsigned e, int off) {
+  double v[FG_MAX];
+#pragma unroll
+  for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < G ? ld_wtd(r, slot(mm, e) + off) : 0.0;
+  double s = 0.0;
+#pragma unroll
+  for (int mm = 0; mm < FG_MAX; ++mm) if (mm < G) s += v[mm];
+  return s;
+}
+template <typename Slot>
+__device__ __forceinline__ float sum_members_f(__amdgpu_buffer_rsrc_t r, const Slot& slot, int G, unsigned e, int off) {
+  float v[FG_MAX];
+#pragma unroll
+  for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < G ? ld_wt1(r, slot(mm, e) + off) : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int mm = 0; mm < FG_MAX; ++mm) if (mm < G) s += v[mm];
+  return s;
+}
+
 __device__ __forceinline__ float4 dd_as_f4(double a, double b) {
   const unsigned long long x = __builtin_bit_cast(unsigned long long, a), y = __builtin_bit_cast(unsigned long long, b);
   return make_float4(__builtin_bit_cast(float, (unsigned)x), __builtin_bit_cast(float, (unsigned)(x >> 32)),
@@ -136,18 +159,24 @@ struct Xchg {
   // thread 0 waits for every other member's flag of epoch e; the caller then barriers
   __device__ void wait(unsigned e) {
     if (threadIdx.x != 0 || failed) return;
-    for (int m = 0; m < G; ++m) {
-      if (m == g) continue;
-      const unsigned* f = flags + (size_t)(base + m) * 2 + (e & 1);
-      unsigned spins = 0;
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 1023u) == 0 &&
-            (spins > (1u << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          failed = true;
-          return;
+    // every member's flag loaded in one pass (independent loads in flight together), until all >= e
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int m = 0; m < FG_MAX; ++m) {
+        if (m < G && m != g) {
+          const unsigned* f = flags + (size_t)(base + m) * 2 + (e & 1);
+          ok = (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e) && ok;
         }
+      }
+      if (ok) return;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 1023u) == 0 &&
+          (spins > (1u << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        failed = true;
+        return;
       }
     }
   }
@@ -267,6 +296,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const int ngroups = gridDim.x / G;
   Xchg xc{rsrc_of(a.pay), a.flags, a.err, grp * G, G, g, 0u, false, false};
   const __amdgpu_buffer_rsrc_t pr = xc.pay;
+  auto xslot = [&](int mm, unsigned e) { return xc.slot(mm, e); };
   // epoch 1: the members' XCD ids (write-through protocol); if the whole group shares one XCD, every later
   // hand-off keeps its bytes in that XCD's L2 (correct for any placement: checked, not assumed)
   {
@@ -392,7 +422,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         ld_chan(pm + PB_BE1, CH, pb);
         if (tid < 2) {
           double s = 0.0;
-          for (int mm = 0; mm < G; ++mm) s += ld_wtd(pr, xc.slot(mm, e) + 2 * tid);
+          s = sum_members_d(pr, xslot, G, e, 2 * tid);
           sm.dred[8 + tid] = s;
         }
         // halo rows from the neighbours (raw conv1d outputs)
@@ -471,7 +501,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(6);
       if (tid < 2) {
         double s = 0.0;
-        for (int mm = 0; mm < G; ++mm) s += ld_wtd(pr, xc.slot(mm, e2) + 2 * tid);
+        s = sum_members_d(pr, xslot, G, e2, 2 * tid);
         sm.dred[8 + tid] = s;
       }
       __syncthreads();
@@ -522,7 +552,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the channel axis)
         if (tid < CH) {
           float s = 0.f;
-          for (int mm = 0; mm < G; ++mm) s += ld_wt1(pr, xc.slot(mm, e) + tid);
+          s = sum_members_f(pr, xslot, G, e, tid);
           sm.vec[tid + 4] = s / (float)T;
           if (tid < 4) { sm.vec[tid] = 0.f; sm.vec[CH + 4 + tid] = 0.f; sm.yf[tid] = 0.f; sm.yf[CH + 4 + tid] = 0.f; }
         } else if (tid < CH + FR + 8) {
@@ -600,7 +630,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         if constexpr (LM == LD_RECURSIVE) { ld_chan(pm + PB_LNBG, CH, pgb); ld_chan(pm + PB_LNBB, CH, pbb); }
         if (tid < NMOM) {
           double s = 0.0;
-          for (int mm = 0; mm < G; ++mm) s += ld_wtd(pr, xc.slot(mm, e) + 2 * tid);
+          s = sum_members_d(pr, xslot, G, e, 2 * tid);
           sm.dred[tid] = s;
         }
         __syncthreads();
