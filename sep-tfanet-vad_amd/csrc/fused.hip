@@ -353,6 +353,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     __syncthreads();
 
     for (int bi = 0; bi < a.nblk; ++bi) {
+      // Opaque per-iteration copies of the lane's row offset and channel: every per-row LDS address is then
+      // base + immediate offset. Without this hipcc hoists the 16 row addresses of each array out of the
+      // block loop as invariants, runs out of registers and spills them (scratch reloads on every row).
+      int hl4o = 4 * hl, mo_ = 32 * wave + (lane & 31);
+      asm volatile("" : "+v"(hl4o), "+v"(mo_));
+      const int m = mo_;
+      auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
       const __half* wb = a.wfrag + (size_t)bi * WF_BLOCK;
       const int li = bi % a.layer;
@@ -598,10 +605,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int tl = trow(r);
-          if (t0 + tl >= T) continue;
-          const float rp = tf ? rv[r] * (afm * sm.at[tl]) : rv[r];
+          const float vm = (t0 + tl < T) ? 1.f : 0.f;  // masked, not branched
+          const float rp = vm * (tf ? rv[r] * (afm * sm.at[tl]) : rv[r]);
           if constexpr (LM == LD_RECURSIVE) {
-            const float ov = o[r], uv = ov + rp;
+            const float ov = vm * o[r], uv = ov + rp;
             mo[0] += ov; mo[1] += ov * ov; mo[2] += uv; mo[3] += uv * uv; mo[4] += be * ov; mo[5] += ga * uv;
             mo[6] += ga * ov * uv; mo[7] += ga * ov; mo[8] += ga * be * uv; mo[9] += ga * ga * uv * uv; mo[10] += ga * ga * uv;
           } else {
