@@ -118,9 +118,9 @@ struct sepvad_model {
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU)
   __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered weights
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
-  float* tpay = nullptr;        // hand-off payload slots [tcn_cap][2][FPAY]
-  unsigned* tflags = nullptr;   // [tcn_cap][2] flags + err word, zeroed before every launch
-  size_t tflag_bytes = 0;
+  unsigned long long* tgran = nullptr;  // hand-off words [tcn_cap][2][NGR]
+  unsigned* terr = nullptr;     // give-up flag of the last launches
+  unsigned tsalt = 0;           // launch counter (hand-off tag salt)
   bool last_fused = false;
   unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
   // timing
@@ -358,10 +358,10 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->tprm, pb.size() * sizeof(float)));
   HIPCHK(hipMemcpy(h->tprm, pb.data(), pb.size() * sizeof(float), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&h->tpay, (size_t)h->tcn_cap * 2 * FPAY * sizeof(float)));
-  h->tflag_bytes = ((size_t)h->tcn_cap * 2 + 16) * sizeof(unsigned);  // multiple of 16 bytes
-  HIPCHK(hipMalloc(&h->tflags, h->tflag_bytes));
-  HIPCHK(hipMemset(h->tflags, 0, h->tflag_bytes));
+  HIPCHK(hipMalloc(&h->tgran, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(h->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&h->terr, 16));
+  HIPCHK(hipMemset(h->terr, 0, 16));
   return SEPVAD_OK;
 }
 
@@ -627,7 +627,7 @@ namespace {
 // the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G && h->tflags != nullptr;
+  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G && h->tgran != nullptr;
 }
 
 // Per-forward timing state (sepvad_set_timing): HIP events around the GEMM launches of chunk 0.
@@ -678,44 +678,63 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
   const bool use_fused = fused_ok(h, T);
   h->last_fused = use_fused;
   if (use_fused) {
-    // one persistent launch for all blocks (fused.hip), then the head GEMM on its output
-    HIPCHK(hipMemsetAsync(h->tflags, 0, h->tflag_bytes, s));
+    // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
     TcnArgs ta{};
-    ta.B = B; ta.T = T; ta.Tp = Tp; ta.G = G; ta.nblk = h->nblk; ta.layer = c.layer;
+    ta.T = T; ta.Tp = Tp; ta.G = G; ta.nblk = h->nblk; ta.layer = c.layer;
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
-    ta.wfrag = h->twf; ta.prm = h->tprm; ta.S0 = w.S0;
-    ta.ln = gn_src(w.rec_gate, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
+    ta.wfrag = h->twf; ta.prm = h->tprm;
     ta.alpha_h = h->out_a;
-    ta.Xfin = w.O[0]; ta.rec_head = w.rec_hs;
+    ta.gran = h->tgran; ta.err = h->terr;
     ta.xmode = getenv("SEPVAD_TCN_XMODE") ? atoi(getenv("SEPVAD_TCN_XMODE")) : 0;
-    ta.pay = h->tpay; ta.flags = h->tflags; ta.err = h->tflags + (size_t)h->tcn_cap * 2;
     int ngroups = std::min(B, h->tcn_cap / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;
+    // epochs per launch and group: 1 (XCD ids) + 4 per block per utterance, < 2^TCN_EPOCH_BITS
+    const int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / (4 * h->nblk);
+    if (max_iter < 1) return fail(SEPVAD_E_ARG, "fused TCN: too many blocks");
+    const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
     const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16;
-    if (probe_path) {
-      if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
-      HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
-      ta.probe = h->tprobe;
-    }
-    if (ev()) return SEPVAD_E_HIP;
-    HIPCHK(launch_tcn(ta, ngroups * G, s));
-    if (ev()) return SEPVAD_E_HIP;
-    if (probe_path) {  // diagnostics only: synchronous dump {grid, nblk, G, T} + stamps
-      std::vector<unsigned long long> hp(probe_n);
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipMemcpy(hp.data(), h->tprobe, probe_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      if (FILE* f = fopen(probe_path, "wb")) {
-        const long long hdr[4] = {(long long)ngroups * G, h->nblk, G, T};
-        fwrite(hdr, sizeof(hdr), 1, f);
-        fwrite(hp.data(), sizeof(unsigned long long), (size_t)ngroups * G * h->nblk * 16, f);
-        fclose(f);
+    for (int u0 = 0; u0 < B; u0 += per_launch) {
+      const int Bl = std::min(per_launch, B - u0);
+      const int ng = std::min(ngroups, Bl);
+      const int ngl = ng >= 8 ? ng - ng % 8 : ng;
+      // tag salt: never 0; hand-off words re-zeroed when the 20-bit salt wraps
+      h->tsalt = (h->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
+      if (h->tsalt == 0) {
+        HIPCHK(hipMemsetAsync(h->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
+        h->tsalt = 1;
       }
-    }
-    if (tr) {
-      tr->gemm_ev.push_back((int)h->ev.size() - 2);
-      tr->g2_ev.push_back((int)h->ev.size() - 2);
+      ta.tag0 = h->tsalt << TCN_EPOCH_BITS;
+      ta.B = Bl;
+      ta.S0 = w.S0 + (size_t)u0 * Tp * CH;
+      ta.ln = gn_src(w.rec_gate + (size_t)u0 * (Tp / GATE_ROWS) * 2, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
+      ta.Xfin = w.O[0] + (size_t)u0 * Tp * CH;
+      ta.rec_head = w.rec_hs + (size_t)u0 * G * 2;
+      ta.probe = nullptr;
+      if (probe_path && u0 == 0) {
+        if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
+        ta.probe = h->tprobe;
+      }
+      if (ev()) return SEPVAD_E_HIP;
+      HIPCHK(launch_tcn(ta, ngl * G, s));
+      if (ev()) return SEPVAD_E_HIP;
+      if (tr) {
+        tr->gemm_ev.push_back((int)h->ev.size() - 2);
+        tr->g2_ev.push_back((int)h->ev.size() - 2);
+      }
+      if (ta.probe) {  // diagnostics only: synchronous dump {grid, nblk, G, T} + stamps
+        std::vector<unsigned long long> hp(probe_n);
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(hp.data(), h->tprobe, probe_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(probe_path, "wb")) {
+          const long long hdr[4] = {(long long)ngl * G, h->nblk, G, T};
+          fwrite(hdr, sizeof(hdr), 1, f);
+          fwrite(hp.data(), sizeof(unsigned long long), (size_t)ngl * G * h->nblk * 16, f);
+          fclose(f);
+        }
+      }
     }
     GemmArgs g{};
     g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
@@ -954,11 +973,14 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
   DeviceGuard dg(h->device);
   if (used) *used = h->last_fused ? 1 : 0;
-  if (!h->tflags) return SEPVAD_OK;
+  if (!h->terr) return SEPVAD_OK;
   HIPCHK(hipDeviceSynchronize());
   unsigned err = 0;
-  HIPCHK(hipMemcpy(&err, h->tflags + (size_t)h->tcn_cap * 2, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up (outputs invalid)");
+  HIPCHK(hipMemcpy(&err, h->terr, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) {
+    HIPCHK(hipMemset(h->terr, 0, 16));
+    return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up (outputs invalid)");
+  }
   return SEPVAD_OK;
 }
 
@@ -1086,8 +1108,8 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->twf) (void)hipFree(h->twf);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
-  if (h->tpay) (void)hipFree(h->tpay);
-  if (h->tflags) (void)hipFree(h->tflags);
+  if (h->tgran) (void)hipFree(h->tgran);
+  if (h->terr) (void)hipFree(h->terr);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);
   delete h;

@@ -19,16 +19,18 @@
 // the multi-kernel path. GroupNorm statistics: float partials per wave, double across waves and members,
 // fixed order => bitwise reproducible and independent of placement and batch composition.
 //
-// Hand-off protocol (MI355X_MICROARCH.md visibility table, row "one lane of each storing workgroup";
-// cdna_hip_programming.md Guideline 16 R1): wave 0 stores the payload write-through (sc1 buffer stores),
-// drains (s_waitcnt vmcnt(0)), then lane 0 stores the epoch into the member's flag (agent-scope relaxed
-// atomic store = sc1). Consumers: thread 0 polls the other members' flags (relaxed sc1 loads + s_sleep,
-// bounded: a give-up sets *err and the kernel runs to completion instead of hanging), a workgroup barrier,
-// then EVERY load of handed-off bytes is an sc1 buffer load. Payload slots are double-buffered by epoch
-// parity: a member publishes epoch e+2 only after it has seen every member's epoch e+1 flag, and every
-// member publishes e+1 only after it has read all epoch-e data.
+// Hand-off protocol (cdna_hip_programming.md Guideline 16 R2, "data is its own flag"): every handed-off
+// 32-bit value travels as one 8-byte word {tag, value} written by a single 64-bit store, so a reader that
+// sees the tag also sees the value (no payload/flag ordering, no drain before a flag). tag = launch salt
+// << 12 | epoch (host: a fresh salt per launch, words zeroed once at create and when the salt wraps).
+// Consumers poll exactly the words they need with agent-scope relaxed loads (L1 bypass), all words of a
+// pass in flight together, bounded (a give-up sets *err and the kernel runs to completion instead of
+// hanging). Stores: when all members of a group report the same XCD (HW_REG_XCC_ID, exchanged at epoch
+// 1) plain stores suffice — the XCD's L2 is the coherence point — else agent-scope (sc1) write-through.
+// Slots are double-buffered by epoch parity: every phase consumes a word of every member, so a member
+// writes epoch e+2 only after every member has written e+1, which each does after its epoch-e reads.
 //
-// Residency: one 512-thread workgroup per CU (LDS ~114 KB), grid <= the occupancy-derived capacity, and a
+// Residency: one 512-thread workgroup per CU (LDS ~158 KB), grid <= the occupancy-derived capacity, and a
 // group's members are dealt to one XCD (blocks b, b+8, ... share an XCD under round-robin dispatch:
 // speed only, never correctness). Groups loop over utterances (persistent), so any batch size runs.
 #include "device_common.h"
@@ -57,7 +59,9 @@ struct TcnSmem {
   float yf[CH + 8];
   float mC[FR + 8], yt[FR + 8], at[FR];
   float cs[FR][8];                // per-frame channel partial sums (8 channel slices)
+  float csum[FR];                 // own per-frame channel sums
   float red[NMOM * 16];
+  unsigned gw[FG_MAX * 2 * NMOM]; // gathered statistic words of all members
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
@@ -79,108 +83,58 @@ __device__ __forceinline__ float unif(float x) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uni(p)), (short)0, 0x7fffffff, 0x00020000);
 }
-// Write-through (sc1) stores / sc1 loads of hand-off payload, addressed as float offsets from the
-// (wave-uniform) payload base: aux 16 = sc1 on gfx950.
-__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int foff, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, foff * 4, 0, 16);
+typedef unsigned long long u64;
+// ---- hand-off words: 8-byte {tag, value} granules (the data is its own flag) ----
+// Same-XCD groups: plain stores keep the words in the XCD's shared L2; otherwise agent-scope (sc1)
+// write-through stores. Consumers always load with agent-scope relaxed atomics (sc1: L1 bypass).
+__device__ __forceinline__ void gput(u64* p, unsigned tag, unsigned v, bool l2) {
+  const u64 w = ((u64)tag << 32) | v;
+  if (l2) __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Same-XCD groups: plain stores keep the line in the shared L2, where the consumers' sc1 loads (L1
-// bypass) find it; the drain before the flag makes the stores complete at L2 first.
-__device__ __forceinline__ void st_l2(__amdgpu_buffer_rsrc_t r, int foff, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, foff * 4, 0, 0);
+__device__ __forceinline__ void gputf(u64* p, unsigned tag, float v, bool l2) {
+  gput(p, tag, __builtin_bit_cast(unsigned, v), l2);
 }
-__device__ __forceinline__ float4 ld_wt(__amdgpu_buffer_rsrc_t r, int foff) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, foff * 4, 0, 16));
+__device__ __forceinline__ void gputd(u64* p, unsigned tag, double v, bool l2) {  // two consecutive words
+  const u64 b = __builtin_bit_cast(u64, v);
+  gput(p, tag, (unsigned)b, l2);
+  gput(p + 1, tag, (unsigned)(b >> 32), l2);
 }
-__device__ __forceinline__ float ld_wt1(__amdgpu_buffer_rsrc_t r, int foff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, foff * 4, 0, 16));
+__device__ __forceinline__ double dword2(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
 }
-__device__ __forceinline__ double ld_wtd(__amdgpu_buffer_rsrc_t r, int foff) {  // foff even
-  const unsigned lo = __builtin_amdgcn_raw_buffer_load_b32(r, foff * 4, 0, 16);
-  const unsigned hi = __builtin_amdgcn_raw_buffer_load_b32(r, foff * 4 + 4, 0, 16);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-// Sum over the group's members (in member order) of the double / float at float offset `off` of each
-// member's slot of epoch e: all loads issued before the first add (one latency, not G).
-template <typename Slot>
-__device__ __forceinline__ double sum_members_d(__amdgpu_buffer_rsrc_t r, const Slot& slot, int G, unsigned e, int off) {
-  double v[FG_MAX];
+// Poll the N words p[k] (nullptr = none) until every tag equals `tag`; values into v[k]. All loads of a
+// pass are in flight together. Bounded: gives up (sets *err) after ~2^20 passes or once *err is set, and
+// the launch then runs to completion with invalid outputs instead of hanging.
+template <int N>
+__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], unsigned* err) {
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
 #pragma unroll
-  for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < G ? ld_wtd(r, slot(mm, e) + off) : 0.0;
-  double s = 0.0;
-#pragma unroll
-  for (int mm = 0; mm < FG_MAX; ++mm) if (mm < G) s += v[mm];
-  return s;
-}
-template <typename Slot>
-__device__ __forceinline__ float sum_members_f(__amdgpu_buffer_rsrc_t r, const Slot& slot, int G, unsigned e, int off) {
-  float v[FG_MAX];
-#pragma unroll
-  for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < G ? ld_wt1(r, slot(mm, e) + off) : 0.f;
-  float s = 0.f;
-#pragma unroll
-  for (int mm = 0; mm < FG_MAX; ++mm) if (mm < G) s += v[mm];
-  return s;
-}
-
-__device__ __forceinline__ float4 dd_as_f4(double a, double b) {
-  const unsigned long long x = __builtin_bit_cast(unsigned long long, a), y = __builtin_bit_cast(unsigned long long, b);
-  return make_float4(__builtin_bit_cast(float, (unsigned)x), __builtin_bit_cast(float, (unsigned)(x >> 32)),
-                     __builtin_bit_cast(float, (unsigned)y), __builtin_bit_cast(float, (unsigned)(y >> 32)));
-}
-
-// Group hand-off state of one workgroup (see the header comment).
-struct Xchg {
-  __amdgpu_buffer_rsrc_t pay; // payload slots [ngroups*G][2][FPAY]
-  unsigned* flags;           // [ngroups*G][2]
-  unsigned* err;
-  int base, G, g;            // first member's index, members, own member index
-  unsigned ep;               // epochs published so far
-  bool failed;               // thread 0: a wait gave up (skip later waits)
-  bool l2;                   // every member on this workgroup's XCD: payload and flags stay in its L2
-
-  __device__ void store(int foff, float4 v) const {
-    if (l2) st_l2(pay, foff, v);
-    else st_wt(pay, foff, v);
-  }
-  __device__ int slot(int member, unsigned e) const { return ((base + member) * 2 + (int)(e & 1)) * FPAY; }
-  // after wave 0 stored the payload of epoch ep+1 into slot(g, ep+1): drain, flag
-  __device__ void publish(int wave, int lane) {
-    ++ep;
-    if (wave == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned* f = flags + (size_t)(base + g) * 2 + (ep & 1);
-      if (lane == 0) {
-        if (l2) *reinterpret_cast<volatile unsigned*>(f) = ep;
-        else __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < N; ++k) {
+      if (p[k] != nullptr) {
+        const u64 x = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = (unsigned)x;
+        ok = ok && (unsigned)(x >> 32) == tag;
       }
     }
-  }
-  // thread 0 waits for every other member's flag of epoch e; the caller then barriers
-  __device__ void wait(unsigned e) {
-    if (threadIdx.x != 0 || failed) return;
-    // every member's flag loaded in one pass (independent loads in flight together), until all >= e
-    unsigned spins = 0;
-    for (;;) {
-      bool ok = true;
-#pragma unroll
-      for (int m = 0; m < FG_MAX; ++m) {
-        if (m < G && m != g) {
-          const unsigned* f = flags + (size_t)(base + m) * 2 + (e & 1);
-          ok = (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e) && ok;
-        }
-      }
-      if (ok) return;
-      __builtin_amdgcn_s_sleep(1);
-      if ((++spins & 1023u) == 0 &&
-          (spins > (1u << 22) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        failed = true;
-        return;
-      }
+    if (ok) return;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0 &&
+        (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
     }
   }
-};
+}
+// granule word layout of one slot
+constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq hi}; P4: 11 doubles as 22 words
+constexpr int GW_TOP = 4;           // P1: rows 0..dil-1      [dil][256]
+constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
+constexpr int GW_ROW = 0;           // P3: per-channel sums over own frames [256]
+constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
+static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // conv1d / res_out GEMM of one wave: acc[32 frames x 32 channels] += A[32 x 16*NS] * W^T. A comes from
 // LDS (hi/lo planes, row stride LDA); the W fragments stream from global (buffer loads over the
@@ -294,24 +248,24 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     g = blockIdx.x % G;
   }
   const int ngroups = gridDim.x / G;
-  Xchg xc{rsrc_of(a.pay), a.flags, a.err, grp * G, G, g, 0u, false, false};
-  const __amdgpu_buffer_rsrc_t pr = xc.pay;
-  auto xslot = [&](int mm, unsigned e) { return xc.slot(mm, e); };
-  // epoch 1: the members' XCD ids (write-through protocol); if the whole group shares one XCD, every later
-  // hand-off keeps its bytes in that XCD's L2 (correct for any placement: checked, not assumed)
+  // hand-off slots of this group: member mm, epoch e -> NGR words; tags a.tag0 + epoch
+  u64* const gbase = a.gran + (size_t)grp * G * 2 * NGR;
+  auto slot = [&](int mm, unsigned e) -> u64* { return gbase + ((size_t)mm * 2 + (e & 1)) * NGR; };
+  unsigned ep = 1;  // epochs published so far (identical sequence in every member); epoch 1 = XCD ids
+  // epoch 1: the members' XCD ids (write-through); if the whole group shares one XCD, every later
+  // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
+  bool l2;
   {
     const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
-    if (tid == 0) st_wt(pr, xc.slot(g, 1), make_float4(__builtin_bit_cast(float, xcc), 0.f, 0.f, 0.f));
-    xc.publish(wave, lane);
-    xc.wait(1);
+    if (tid == 0) gput(slot(g, 1), a.tag0 + 1, xcc, false);
+    const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
+    unsigned v[1];
+    gpoll<1>(p, a.tag0 + 1, v, a.err);
+    if (tid < G) sm.gw[tid] = v[0];
     __syncthreads();
-    if (tid == 0) {
-      bool same = a.xmode == 0;
-      for (int mm = 0; mm < G; ++mm) same = same && __builtin_bit_cast(unsigned, ld_wt1(pr, xc.slot(mm, 1))) == xcc;
-      sm.red[0] = same ? 1.f : 0.f;
-    }
-    __syncthreads();
-    xc.l2 = sm.red[0] != 0.f;
+    bool same = a.xmode == 0;
+    for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
+    l2 = same;
     __syncthreads();
   }
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
@@ -376,6 +330,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (idx < PB_SIZE / 4) pv[k] = src[idx];
         }
       }
+      const unsigned e1 = ++ep, tag1 = a.tag0 + e1;
       // ================= conv1d 256->256 (model/model.py:132) + PReLU =================
       f32x16v acc;
 #pragma unroll
@@ -392,6 +347,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         __syncthreads();
         const float ws = pm[PB_WS1 + m], bias = pm[PB_B1 + m], a1 = pm[PB_A1];
+        u64* s1 = slot(g, e1);
         float st[2] = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -400,55 +356,55 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           v = (t0 + tl < T) ? v : 0.f;
           sm.H[(tl + 4) * CH + m] = v;
           st[0] += v; st[1] += v * v;
+          if (r < 4 && hl == 0 && tl < dil) gputf(s1 + GW_TOP + tl * CH + m, tag1, v, l2);
+          if (r >= 12 && hl == 1 && tl >= FR - dil) gputf(s1 + GW_BOT + (tl - (FR - dil)) * CH + m, tag1, v, l2);
         }
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H complete
+        if (tid < 2) gputd(s1 + GW_STAT + 2 * tid, tag1, sm.dred[tid], l2);
       TPROBE(2);
       }
-      // ---- P1: GN1 partial sums + boundary rows (first dil / last dil own frames) ----
+      // ---- consume P1: neighbours' boundary rows -> H halo; every member's GN1 sums ----
       {
-        const unsigned e = xc.ep + 1;
-        const int dst = xc.slot(g, e);
-        __syncthreads();
-        if (wave == 0) {
-          if (lane == 0) xc.store(dst + 0, dd_as_f4(sm.dred[0], sm.dred[1]));
-          // rows 0..dil-1 -> [16, 16 + dil*256); rows 32-dil..31 -> [16 + 4*256, ...)
-          for (int i = lane; i < 2 * dil * (CH / 4); i += 64) {
-            const int j = i / (CH / 4), c4 = (i % (CH / 4)) * 4;
-            const int tl = j < dil ? j : FR - 2 * dil + j;
-            const int off = j < dil ? 16 + j * CH : 16 + 4 * CH + (j - dil) * CH;
-            xc.store(dst + off + c4, *reinterpret_cast<const float4*>(&sm.H[(tl + 4) * CH + c4]));
+        const u64* p[5];
+        unsigned v[5];
+        int hrow[4], hcol[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = tid + k * NTHR;
+          p[k] = nullptr;
+          hrow[k] = -1; hcol[k] = 0;
+          if (i < 2 * dil * CH) {
+            const int j = i / CH, c = i % CH;
+            hcol[k] = c;
+            if (j < dil) {          // frames -dil..-1: predecessor's last dil rows
+              hrow[k] = 4 - dil + j;
+              if (g > 0) p[k] = slot(g - 1, e1) + GW_BOT + j * CH + c;
+            } else {                // frames 32..32+dil-1: successor's first dil rows
+              hrow[k] = 4 + FR + (j - dil);
+              if (g + 1 < G) p[k] = slot(g + 1, e1) + GW_TOP + (j - dil) * CH + c;
+            }
           }
         }
-        xc.publish(wave, lane);
-        xc.wait(e);
-        __syncthreads();
+        const int sk = tid - (NTHR - 4 * G);  // last 4G threads: GN1 words of member sk/4
+        p[4] = sk >= 0 ? slot(sk >> 2, e1) + GW_STAT + (sk & 3) : nullptr;
+        gpoll<5>(p, tag1, v, a.err);
       TPROBE(3);
-        // GN1 statistics over the group (members in order) -> affine
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (hrow[k] >= 0) sm.H[hrow[k] * CH + hcol[k]] = p[k] != nullptr ? __builtin_bit_cast(float, v[k]) : 0.f;
+        if (sk >= 0) sm.gw[sk] = v[4];
+        // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
+        // order, so no wait above sits behind the weight stream)
+        prefetch_w(rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl);
         float pg[2], pb[2];
         ld_chan(pm + PB_G1, CH, pg);
         ld_chan(pm + PB_BE1, CH, pb);
+        __syncthreads();
         if (tid < 2) {
           double s = 0.0;
-          s = sum_members_d(pr, xslot, G, e, 2 * tid);
+          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[4 * mm + 2 * tid], sm.gw[4 * mm + 2 * tid + 1]);
           sm.dred[8 + tid] = s;
         }
-        // halo rows from the neighbours (raw conv1d outputs)
-        for (int i = tid; i < 2 * dil * (CH / 4); i += NTHR) {
-          const int j = i / (CH / 4), c4 = (i % (CH / 4)) * 4;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          int row;
-          if (j < dil) {  // rows -dil..-1 = predecessor's last dil rows
-            row = 4 - dil + j;
-            if (g > 0) v = ld_wt(pr, xc.slot(g - 1, e) + 16 + 4 * CH + j * CH + c4);
-          } else {        // rows 32..32+dil-1 = successor's first dil rows
-            row = 4 + FR + (j - dil);
-            if (g + 1 < G) v = ld_wt(pr, xc.slot(g + 1, e) + 16 + (j - dil) * CH + c4);
-          }
-          *reinterpret_cast<float4*>(&sm.H[row * CH + c4]) = v;
-        }
-        // res_out weights: in flight during the depthwise conv (issued after every load this phase
-        // waits for: vmcnt retires in order, so nothing earlier waits behind the weight stream)
-        prefetch_w(rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl);
         __syncthreads();
         gn_affine(sm.dred + 8, CH, T, 1e-8f, pg, pb, sm.c[0], sm.c[1]);
         __syncthreads();
@@ -489,13 +445,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
       }
-      // ---- P2: GN2 partial sums (awaited after the res_out main loop) ----
-      const unsigned e2 = xc.ep + 1;
-      {
-        __syncthreads();
-        if (wave == 0 && lane == 0) xc.store(xc.slot(g, e2), dd_as_f4(sm.dred[0], sm.dred[1]));
-        xc.publish(wave, lane);
-      }
+      // ---- P2 words: GN2 partial sums (awaited after the res_out main loop) ----
+      const unsigned e2 = ++ep, tag2 = a.tag0 + e2;
+      if (tid < 2) gputd(slot(g, e2) + GW_STAT + 2 * tid, tag2, sm.dred[tid], l2);
       // ================= res_out 512->256 (model/model.py:136,144) with reg2 folded =================
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -503,16 +455,22 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         wave_gemm<NS2, LDD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
-      xc.wait(e2);
-      __syncthreads();  // also: every wave is done reading d from LDS
+      {
+        const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
+        unsigned v[1];
+        gpoll<1>(p, tag2, v, a.err);
+        if (tid < 4 * G) sm.gw[tid] = v[0];
+        __syncthreads();  // also: every wave is done reading d from LDS
       TPROBE(6);
-      if (tid < 2) {
-        double s = 0.0;
-        s = sum_members_d(pr, xslot, G, e2, 2 * tid);
-        sm.dred[8 + tid] = s;
+        if (tid < 2) {
+          double s = 0.0;
+          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[4 * mm + 2 * tid], sm.gw[4 * mm + 2 * tid + 1]);
+          sm.dred[8 + tid] = s;
+        }
+        __syncthreads();
       }
-      __syncthreads();
       f32x16v& rv = acc;  // r = res_out output, in place
+      const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
       {
         float fmu, frs;
         gn_moments(sm.dred[8], sm.dred[9], (double)HID * T, 1e-8f, fmu, frs);
@@ -529,51 +487,54 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             if ((lane & 31) == 31) sm.cs[tl][wave] = cs;
           }
         }
-        if (tf) {
+        if (tf) {  // P3 words: per-channel sums over own frames (a_f)
           rsum += __shfl_xor(rsum, 32);
-          if (hl == 0) sm.vec[m] = rsum;
+          if (hl == 0) gputf(slot(g, e3) + GW_ROW + m, tag3, rsum, l2);
         }
       }
-      // ---- TF_Attention (model/model.py:182-208): P3 = channel sums over own frames + per-frame sums ----
+      // ---- TF_Attention (model/model.py:182-208) ----
       if (tf) {
         __syncthreads();
-        if (tid < FR) {
+        if (tid < FR) {  // P3 words: per-frame channel sums (a_t)
           float s = 0.f;
 #pragma unroll
           for (int sl = 0; sl < 8; ++sl) s += sm.cs[tid][sl];
-          sm.mC[tid] = s;   // staging (own frame channel sums)
+          sm.csum[tid] = s;
+          gputf(slot(g, e3) + GW_COL + tid, tag3, s, l2);
         }
-        __syncthreads();
       TPROBE(7);
-        const unsigned e = xc.ep + 1;
-        if (wave == 0) {
-          const int dst = xc.slot(g, e);
-          xc.store(dst + 4 * lane, *reinterpret_cast<const float4*>(&sm.vec[4 * lane]));     // [0, 256)
-          if (lane < FR / 4) xc.store(dst + CH + 4 * lane, *reinterpret_cast<const float4*>(&sm.mC[4 * lane]));
+        // consume P3: rowsums of every member (a_f), channel sums of the 4 frames either side (a_t)
+        {
+          const u64* pp[FG_MAX];
+          unsigned v[FG_MAX];
+#pragma unroll
+          for (int mm = 0; mm < FG_MAX; ++mm) pp[mm] = (tid < CH && mm < G) ? slot(mm, e3) + GW_ROW + tid : nullptr;
+          int mi = -1;  // a_t input index (frame t0 - 4 + mi) served by this thread
+          if (tid >= CH && tid < CH + 8) {
+            const int k = tid - CH;
+            mi = k < 4 ? k : FR + k;             // 0..3 and 36..39
+            const int tl = mi - 4, t = t0 + tl;
+            if (t >= 0 && t < T) pp[0] = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
+          }
+          gpoll<FG_MAX>(pp, tag3, v, a.err);
+          __syncthreads();  // csum complete (read below by other threads)
+          if (tid < CH) {
+            float s = 0.f;
+            for (int mm = 0; mm < G; ++mm) s += __builtin_bit_cast(float, v[mm]);
+            sm.vec[tid + 4] = s / (float)T;
+            if (tid < 4) { sm.vec[tid] = 0.f; sm.vec[CH + 4 + tid] = 0.f; sm.yf[tid] = 0.f; sm.yf[CH + 4 + tid] = 0.f; }
+          } else if (mi >= 0) {
+            sm.mC[mi] = pp[0] != nullptr ? __builtin_bit_cast(float, v[0]) / (float)CH : 0.f;
+          } else if (tid >= CH + 8 && tid < CH + 8 + FR) {
+            const int tl = tid - CH - 8;
+            sm.mC[tl + 4] = (t0 + tl < T) ? sm.csum[tl] / (float)CH : 0.f;
+          }
         }
-        xc.publish(wave, lane);
-        xc.wait(e);
         __syncthreads();
       TPROBE(8);
         const float* p = pm + PB_ATT;
-        // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the channel axis)
-        if (tid < CH) {
-          float s = 0.f;
-          s = sum_members_f(pr, xslot, G, e, tid);
-          sm.vec[tid + 4] = s / (float)T;
-          if (tid < 4) { sm.vec[tid] = 0.f; sm.vec[CH + 4 + tid] = 0.f; sm.yf[tid] = 0.f; sm.yf[CH + 4 + tid] = 0.f; }
-        } else if (tid < CH + FR + 8) {
-          // a_t inputs: channel means of frames t0-4 .. t0+35 (zero outside [0, T))
-          const int i = tid - CH, tl = i - 4, t = t0 + tl;
-          float v = 0.f;
-          if (t >= 0 && t < T) {
-            const int mm = tl < 0 ? g - 1 : (tl >= FR ? g + 1 : g);
-            const int tj = tl < 0 ? tl + FR : (tl >= FR ? tl - FR : tl);
-            v = ld_wt1(pr, xc.slot(mm, e) + CH + tj) / (float)CH;
-          }
-          sm.mC[i] = v;   // index i <-> frame t0 - 4 + i
-        }
-        __syncthreads();
+        // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the channel axis);
+        // a_t: mean over channels -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the frame axis)
         if (tid < CH) {
           sm.yf[tid + 4] = p[11] + p[8] * sm.vec[tid + 3] + p[9] * sm.vec[tid + 4] + p[10] * sm.vec[tid + 5];
         } else if (tid < CH + FR + 8) {
@@ -617,16 +578,16 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         block_sums<NMOM>(mo, sm.red, sm.dred);
       TPROBE(10);
-        // ---- P4 ----
-        const unsigned e = xc.ep + 1;
-        __syncthreads();
-        if (wave == 0 && lane < 6) {
-          const double d0 = sm.dred[2 * lane], d1 = 2 * lane + 1 < NMOM ? sm.dred[2 * lane + 1] : 0.0;
-          xc.store(xc.slot(g, e) + 4 * lane, dd_as_f4(d0, d1));
+        // ---- P4 words: the moment record (11 doubles); consume every member's ----
+        const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
+        if (tid < NMOM) gputd(slot(g, e4) + GW_STAT + 2 * tid, tag4, sm.dred[tid], l2);
+        {
+          const int k = tid;  // word k % 22 of member k / 22
+          const u64* pp[1] = {k < 2 * NMOM * G ? slot(k / (2 * NMOM), e4) + GW_STAT + k % (2 * NMOM) : nullptr};
+          unsigned v[1];
+          gpoll<1>(pp, tag4, v, a.err);
+          if (k < 2 * NMOM * G) sm.gw[k] = v[0];
         }
-        xc.publish(wave, lane);
-        xc.wait(e);
-        __syncthreads();
       TPROBE(11);
         LoadSpec ld{};
         ld.gn.eps = 1e-5f; ld.eps2 = 1e-5f;
@@ -635,9 +596,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float pga[2], pba[2], pgb[2], pbb[2];
         ld_chan(pm + PB_LNAG, CH, pga); ld_chan(pm + PB_LNAB, CH, pba);
         if constexpr (LM == LD_RECURSIVE) { ld_chan(pm + PB_LNBG, CH, pgb); ld_chan(pm + PB_LNBB, CH, pbb); }
+        __syncthreads();
         if (tid < NMOM) {
           double s = 0.0;
-          s = sum_members_d(pr, xslot, G, e, 2 * tid);
+          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[2 * NMOM * mm + 2 * tid], sm.gw[2 * NMOM * mm + 2 * tid + 1]);
           sm.dred[tid] = s;
         }
         __syncthreads();

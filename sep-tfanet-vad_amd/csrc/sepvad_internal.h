@@ -227,7 +227,8 @@ hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 // ---- fused persistent TCN (fused.hip) ----
 constexpr int FR = 32;          // frames per workgroup
 constexpr int FG_MAX = 8;       // workgroups per utterance (T <= 256)
-constexpr int FPAY = 2304;      // floats per hand-off payload slot (>= 16 + 8 * 256)
+constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
+constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
 constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine
 constexpr int PB_WD = 1024, PB_BD = 2560;                          // depthwise [512][3], bias [512]
@@ -248,9 +249,9 @@ struct TcnArgs {
   float alpha_h;         // TCN.output.0 PReLU
   float* Xfin;           // [B][Tp][CH] TCN output x' (head input)
   double* rec_head;      // [B][G][2] (sum, sumsq) of PReLU(x') per member
-  float* pay;            // hand-off payload slots [grid][2][FPAY]
-  unsigned* flags;       // [grid][2] (zeroed before every launch)
-  unsigned* err;         // give-up flag (zeroed with the flags)
+  unsigned long long* gran;  // hand-off words [grid][2][NGR]
+  unsigned tag0;         // launch salt << TCN_EPOCH_BITS (tags of this launch: tag0 + epoch, epoch >= 1)
+  unsigned* err;         // give-up flag (sticky until sepvad_fused_status reads it)
   int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
                          // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
