@@ -181,19 +181,25 @@ __device__ __forceinline__ void gn_affine(const double* acc, int K, int T, float
 //   0 Σo  1 Σo²  2 Σu  3 Σu²  4 Σbe·o  5 Σg·u  6 Σg·o·u  7 Σg·o  8 Σg·be·u  9 Σg²·u²  10 Σg²·u
 // (u = o + r', g = gamma_a[c], be = beta_a[c]); v = (o+be) + ra·g·(u-μa) gives Σv, Σv² in closed
 // form, so neither u nor v is materialized. wsum = {Σg, Σbe, Σbe², Σg·be, Σg²} over channels (host).
-__device__ inline void recursive_affine(const double* m, const LoadSpec& ld, int K, int T, const float (&ga)[2],
-                                        const float (&ba)[2], const float (&gb)[2], const float (&bb)[2], float* c0,
-                                        float* c1, float* c2, float* c3) {
+// (mean, rstd) of GN_a and GN_b from the moment sums (the channel-independent part of recursive_affine).
+__device__ __forceinline__ void recursive_moments(const double* m, const double* wsum, float eps_a, float eps_b,
+                                                  int K, int T, float& mua_f, float& rsa, float& mub_f,
+                                                  float& rsb) {
   const double cnt = (double)K * T, Tn = (double)T;
-  float mua_f, rsa;
-  gn_moments(m[2], m[3], cnt, ld.gn.eps, mua_f, rsa);
+  gn_moments(m[2], m[3], cnt, eps_a, mua_f, rsa);
   const double ra = rsa, mu = mua_f;
-  const double gs = ld.wsum[0], bs = ld.wsum[1], bbs = ld.wsum[2], gbs = ld.wsum[3], ggs = ld.wsum[4];
+  const double gs = wsum[0], bs = wsum[1], bbs = wsum[2], gbs = wsum[3], ggs = wsum[4];
   const double sv = m[0] + ra * (m[5] - mu * Tn * gs) + Tn * bs;
   const double svv = m[1] + 2.0 * m[4] + Tn * bbs + 2.0 * ra * (m[6] - mu * m[7] + m[8] - mu * Tn * gbs) +
                      ra * ra * (m[9] - 2.0 * mu * m[10] + mu * mu * Tn * ggs);
-  float mub_f, rsb;
-  gn_moments(sv, svv, cnt, ld.eps2, mub_f, rsb);
+  gn_moments(sv, svv, cnt, eps_b, mub_f, rsb);
+}
+
+__device__ inline void recursive_affine(const double* m, const LoadSpec& ld, int K, int T, const float (&ga)[2],
+                                        const float (&ba)[2], const float (&gb)[2], const float (&bb)[2], float* c0,
+                                        float* c1, float* c2, float* c3) {
+  float mua_f, rsa, mub_f, rsb;
+  recursive_moments(m, ld.wsum, ld.gn.eps, ld.eps2, K, T, mua_f, rsa, mub_f, rsb);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int k = threadIdx.x + q * blockDim.x;

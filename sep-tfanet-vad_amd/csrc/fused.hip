@@ -183,6 +183,27 @@ __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, int idx,
   lo[idx] = (_Float16)(v - (float)h);
 }
 
+// two adjacent values (idx even): one 32-bit LDS store per plane
+__device__ __forceinline__ void split_store2(_Float16* hi, _Float16* lo, int idx, float v0, float v1) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+  *reinterpret_cast<f16x2*>(hi + idx) = f16x2{h0, h1};
+  *reinterpret_cast<f16x2*>(lo + idx) = f16x2{(_Float16)(v0 - (float)h0), (_Float16)(v1 - (float)h1)};
+}
+
+// GroupNorm affine of the 256 channels, one per thread tid < CH (as device_common.h gn_affine); the
+// parameters are read from the LDS blob here, so nothing is held in registers across the barriers before.
+__device__ __forceinline__ void gn_affine_ch(int tid, const double* acc, int T, float eps, const float* g,
+                                             const float* be, float* s, float* h) {
+  float mu, rs;
+  gn_moments(acc[0], acc[1], (double)CH * T, eps, mu, rs);
+  if (tid < CH) {
+    const float sc = rs * g[tid];
+    s[tid] = sc;
+    h[tid] = be[tid] - sc * mu;
+  }
+}
+
 // diagnostics (SEPVAD_TCN_PROBE): wave 0's wall clock at 13 phase points of every block of the first
 // utterance each workgroup processes: probe[(blockIdx * nblk + block) * 16 + point]
 #define TPROBE(k)                                                                                  \
@@ -310,9 +331,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // Opaque per-iteration copies of the lane's row offset and channel: every per-row LDS address is then
       // base + immediate offset. Without this hipcc hoists the 16 row addresses of each array out of the
       // block loop as invariants, runs out of registers and spills them (scratch reloads on every row).
-      int hl4o = 4 * hl, mo_ = 32 * wave + (lane & 31);
-      asm volatile("" : "+v"(hl4o), "+v"(mo_));
-      const int m = mo_;
+      int hl4o = 4 * hl, mo_ = 32 * wave + (lane & 31), tido = threadIdx.x;
+      asm volatile("" : "+v"(hl4o), "+v"(mo_), "+v"(tido));
+      const int m = mo_, tid = tido, lane = tid & 63;
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
       const __half* wb = a.wfrag + (size_t)bi * WF_BLOCK;
@@ -396,9 +417,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
         prefetch_w(rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl);
-        float pg[2], pb[2];
-        ld_chan(pm + PB_G1, CH, pg);
-        ld_chan(pm + PB_BE1, CH, pb);
         __syncthreads();
         if (tid < 2) {
           double s = 0.0;
@@ -406,8 +424,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sm.dred[8 + tid] = s;
         }
         __syncthreads();
-        gn_affine(sm.dred + 8, CH, T, 1e-8f, pg, pb, sm.c[0], sm.c[1]);
+        gn_affine_ch(tid, sm.dred + 8, T, 1e-8f, pm + PB_G1, pm + PB_BE1, sm.c[0], sm.c[1]);
         __syncthreads();
+      TPROBE(13);
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
@@ -431,6 +450,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = rh0 + i;
           const float x0 = hn(tl - dil), x1 = hn(tl), x2 = hn(tl + dil);
           const bool valid = t0 + tl < T;
+          float dv[2];
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             float x = wv[q][3];
@@ -439,9 +459,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             x = fmaf(wv[q][2], x2, x);
             const float v = valid ? prelu_f(x, a2) : 0.f;
             st[0] += v; st[1] += v * v;
-            split_store(sm.Ahi, sm.Alo, tl * LDD + 2 * c + q, v);
+            dv[q] = v;
           }
+          split_store2(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
         }
+      TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
       }
@@ -589,13 +611,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (k < 2 * NMOM * G) sm.gw[k] = v[0];
         }
       TPROBE(11);
-        LoadSpec ld{};
-        ld.gn.eps = 1e-5f; ld.eps2 = 1e-5f;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) ld.wsum[j] = reinterpret_cast<const double*>(pm + PB_WSUM)[j];
-        float pga[2], pba[2], pgb[2], pbb[2];
-        ld_chan(pm + PB_LNAG, CH, pga); ld_chan(pm + PB_LNAB, CH, pba);
-        if constexpr (LM == LD_RECURSIVE) { ld_chan(pm + PB_LNBG, CH, pgb); ld_chan(pm + PB_LNBB, CH, pbb); }
         __syncthreads();
         if (tid < NMOM) {
           double s = 0.0;
@@ -604,9 +619,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         __syncthreads();
         if constexpr (LM == LD_RECURSIVE) {
-          recursive_affine(sm.dred, ld, CH, T, pga, pba, pgb, pbb, sm.c[0], sm.c[1], sm.c[2], sm.c[3]);
+          float mua, rsa, mub, rsb;
+          recursive_moments(sm.dred, reinterpret_cast<const double*>(pm + PB_WSUM), 1e-5f, 1e-5f, CH, T, mua, rsa,
+                            mub, rsb);
+          if (tid < CH) {  // as recursive_affine, one channel per thread
+            const float sa = rsa * pm[PB_LNAG + tid];
+            sm.c[0][tid] = sa; sm.c[1][tid] = pm[PB_LNAB + tid] - sa * mua;
+            const float sb = rsb * pm[PB_LNBG + tid];
+            sm.c[2][tid] = sb; sm.c[3][tid] = pm[PB_LNBB + tid] - sb * mub;
+          }
         } else {
-          gn_affine(sm.dred + 2, CH, T, 1e-5f, pga, pba, sm.c[0], sm.c[1]);
+          gn_affine_ch(tid, sm.dred + 2, T, 1e-5f, pm + PB_LNAG, pm + PB_LNAB, sm.c[0], sm.c[1]);
         }
         __syncthreads();
       }

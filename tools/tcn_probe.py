@@ -9,6 +9,9 @@ import numpy as np
 
 NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN2 stats", "res_out GEMM",
          "P2 wait", "rowsum/colsum", "P3 publish+wait", "gates", "moments", "P4 publish+wait", "x' update"]
+# sub-phase stamps currently placed in fused.hip: slot 13 after the GN1 affine (dwconv phase start),
+# slot 14 after the depthwise loop (before the GN2 block sums)
+SUB = [(13, 3, "dwconv: GN1 affine"), (14, 13, "dwconv: loop"), (4, 14, "dwconv: GN2 sums")]
 
 
 def main(path):
@@ -25,10 +28,12 @@ def main(path):
     for i, n in enumerate(NAMES):
         v = d[:, 1:, i]  # skip block 0 (cold)
         print(f"  {n:24s} median {np.median(v):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
-    cyc = full[:, 1:, 14] - full[:, 1:, 13]  # shader clock ticks (x100: the array was scaled to us)
-    if (cyc > 0).all():
-
-        print(f"shader clock during the blocks: {np.median(cyc * 100.0 / blk[:, 1:]) / 1e3:.2f} GHz (s_memtime ticks / wall us)")
+    # optional sub-phase stamps (slots 13..15) splitting one phase: (slot, previous stamp, label)
+    for k, prev, label in SUB:
+        v = full[:, 1:, k]
+        if (v > 0).all():
+            dv = v - full[:, 1:, prev]
+            print(f"    {label:22s} median {np.median(dv):6.2f}  p90 {np.percentile(dv, 90):6.2f} us")
 
 
 if __name__ == "__main__":
