@@ -33,6 +33,8 @@
 // Residency: one 512-thread workgroup per CU (LDS ~158 KB), grid <= the occupancy-derived capacity, and a
 // group's members are dealt to one XCD (blocks b, b+8, ... share an XCD under round-robin dispatch:
 // speed only, never correctness). Groups loop over utterances (persistent), so any batch size runs.
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace sepvad {
@@ -417,22 +419,27 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
         prefetch_w(rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl);
-        __syncthreads();
-        if (tid < 2) {
-          double s = 0.0;
-          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[4 * mm + 2 * tid], sm.gw[4 * mm + 2 * tid + 1]);
-          sm.dred[8 + tid] = s;
-        }
-        __syncthreads();
-        gn_affine_ch(tid, sm.dred + 8, T, 1e-8f, pm + PB_G1, pm + PB_BE1, sm.c[0], sm.c[1]);
-        __syncthreads();
-      TPROBE(13);
+        __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
         const int c = tid & (CH - 1), rh0 = (tid >> 8) * (FR / 2);
         const float a2 = pm[PB_A2];
-        const float sc = sm.c[0][c], sh = sm.c[1][c];
+        // GN1 affine of this thread's channel, computed in-thread from the members' sums (member order,
+        // as gn_affine: no LDS round trip, no barrier)
+        float sc, sh;
+        {
+          double acc[2] = {0.0, 0.0};
+          for (int mm = 0; mm < G; ++mm) {
+            acc[0] += dword2(sm.gw[4 * mm], sm.gw[4 * mm + 1]);
+            acc[1] += dword2(sm.gw[4 * mm + 2], sm.gw[4 * mm + 3]);
+          }
+          float mu, rs;
+          gn_moments(acc[0], acc[1], (double)CH * T, 1e-8f, mu, rs);
+          sc = rs * pm[PB_G1 + c];
+          sh = pm[PB_BE1 + c] - sc * mu;
+        }
+      TPROBE(13);
         float wv[2][4];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -440,28 +447,44 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           wv[q][0] = pm[PB_WD + j * 3 + 0]; wv[q][1] = pm[PB_WD + j * 3 + 1]; wv[q][2] = pm[PB_WD + j * 3 + 2];
           wv[q][3] = pm[PB_BD + j];
         }
-        auto hn = [&](int tl) -> float {  // GN1(h) at local frame tl (zero outside [0, T))
-          const int t = t0 + tl;
-          return (t >= 0 && t < T) ? fmaf(sm.H[(tl + 4) * CH + c], sc, sh) : 0.f;
-        };
         float st[2] = {0.f, 0.f};
-#pragma unroll 4
-        for (int i = 0; i < FR / 2; ++i) {
-          const int tl = rh0 + i;
-          const float x0 = hn(tl - dil), x1 = hn(tl), x2 = hn(tl + dil);
-          const bool valid = t0 + tl < T;
-          float dv[2];
+        // rows rh0-D .. rh0+15+D of this channel once into registers (GN1 applied, zero outside [0, T));
+        // H holds rows -4..35, so every load is in bounds and issued unconditionally
+        auto rows = [&](auto DC) {
+          constexpr int D = decltype(DC)::value;
+          float hv[FR / 2 + 2 * D];
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            float x = wv[q][3];
-            x = fmaf(wv[q][0], x0, x);
-            x = fmaf(wv[q][1], x1, x);
-            x = fmaf(wv[q][2], x2, x);
-            const float v = valid ? prelu_f(x, a2) : 0.f;
-            st[0] += v; st[1] += v * v;
-            dv[q] = v;
+          for (int i = 0; i < FR / 2 + 2 * D; ++i) {
+            const int tl = rh0 - D + i, t = t0 + tl;
+            const float x = sm.H[(tl + 4) * CH + c];
+            // multiply by the 0/1 row mask rather than select: a select lets the compiler sink each load
+            // into its own branch (one exposed LDS round trip per row)
+            const float vm = (t >= 0 && t < T) ? 1.f : 0.f;
+            hv[i] = fmaf(x, sc, sh) * vm;
           }
-          split_store2(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
+#pragma unroll
+          for (int i = 0; i < FR / 2; ++i) {
+            const int tl = rh0 + i;
+            const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
+            float dv[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              float x = wv[q][3];
+              x = fmaf(wv[q][0], hv[i], x);
+              x = fmaf(wv[q][1], hv[i + D], x);
+              x = fmaf(wv[q][2], hv[i + 2 * D], x);
+              const float v = prelu_f(x, a2) * vo;
+              st[0] += v; st[1] += v * v;
+              dv[q] = v;
+            }
+            split_store2(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
+          }
+        };
+        switch (dil) {
+          case 1: rows(std::integral_constant<int, 1>{}); break;
+          case 2: rows(std::integral_constant<int, 2>{}); break;
+          case 3: rows(std::integral_constant<int, 3>{}); break;
+          default: rows(std::integral_constant<int, 4>{}); break;
         }
       TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
@@ -484,18 +507,19 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         if (tid < 4 * G) sm.gw[tid] = v[0];
         __syncthreads();  // also: every wave is done reading d from LDS
       TPROBE(6);
-        if (tid < 2) {
-          double s = 0.0;
-          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[4 * mm + 2 * tid], sm.gw[4 * mm + 2 * tid + 1]);
-          sm.dred[8 + tid] = s;
-        }
-        __syncthreads();
       }
       f32x16v& rv = acc;  // r = res_out output, in place
       const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
       {
         float fmu, frs;
-        gn_moments(sm.dred[8], sm.dred[9], (double)HID * T, 1e-8f, fmu, frs);
+        {
+          double s0 = 0.0, s1 = 0.0;  // every member's GN2 sums, member order
+          for (int mm = 0; mm < G; ++mm) {
+            s0 += dword2(sm.gw[4 * mm], sm.gw[4 * mm + 1]);
+            s1 += dword2(sm.gw[4 * mm + 2], sm.gw[4 * mm + 3]);
+          }
+          gn_moments(s0, s1, (double)HID * T, 1e-8f, fmu, frs);
+        }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
         float rsum = 0.f;
 #pragma unroll
