@@ -63,7 +63,7 @@ struct TcnSmem {
   float cs[FR][8];                // per-frame channel partial sums (8 channel slices)
   float csum[FR];                 // own per-frame channel sums
   float red[NMOM * 16];
-  unsigned gw[FG_MAX * 2 * NMOM]; // gathered statistic words of all members
+  unsigned gw[FG_MAX * 2 * NMOM] __attribute__((aligned(8)));  // gathered statistic words of all members
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
@@ -236,15 +236,34 @@ __device__ __forceinline__ float wave_total(float v) {
   v += dpp_f<0x143>(v);
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const u64 b = __builtin_bit_cast(u64, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
+}
+// {sum, sumsq} over the G members' statistic words (member mm: doubles 2mm, 2mm+1 of gw), member order;
+// lanes 0/1 of every wave load and add, the totals are returned wave-uniform
+__device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int lane) {
+  const double* gd = reinterpret_cast<const double*>(gw);
+  const int j = lane & 1;
+  double s = 0.0;
+  for (int mm = 0; mm < G; ++mm) s += gd[2 * mm + j];
+  return double2{readlane_d(s, 0), readlane_d(s, 1)};
+}
 // Block sums of NV per-thread values (512 threads): waves by DPP, the 8 wave totals in double in wave
 // order by thread j < NV into out[j]. One barrier; callers barrier again before reading `out`.
 template <int NV>
 __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* out) {
   const int w = threadIdx.x >> 6;
+  float t[NV];
 #pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const float t = wave_total(v[j]);
-    if ((threadIdx.x & 63) == 0) lds[j * 8 + w] = t;
+  for (int j = 0; j < NV; ++j) {  // independent DPP chains (interleaved by the scheduler); lane 63 = total
+    t[j] = half_total(v[j]);
+    t[j] += dpp_f<0x143>(t[j]);
+  }
+  if ((threadIdx.x & 63) == 63) {  // one branch for all NV stores
+#pragma unroll
+    for (int j = 0; j < NV; ++j) lds[j * 8 + w] = t[j];
   }
   __syncthreads();
   if (threadIdx.x < NV) {
@@ -429,13 +448,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // as gn_affine: no LDS round trip, no barrier)
         float sc, sh;
         {
-          double acc[2] = {0.0, 0.0};
-          for (int mm = 0; mm < G; ++mm) {
-            acc[0] += dword2(sm.gw[4 * mm], sm.gw[4 * mm + 1]);
-            acc[1] += dword2(sm.gw[4 * mm + 2], sm.gw[4 * mm + 3]);
-          }
+          const double2 acc = member_sums2(sm.gw, G, lane);
           float mu, rs;
-          gn_moments(acc[0], acc[1], (double)CH * T, 1e-8f, mu, rs);
+          gn_moments(acc.x, acc.y, (double)CH * T, 1e-8f, mu, rs);
           sc = rs * pm[PB_G1 + c];
           sh = pm[PB_BE1 + c] - sc * mu;
         }
@@ -513,12 +528,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       {
         float fmu, frs;
         {
-          double s0 = 0.0, s1 = 0.0;  // every member's GN2 sums, member order
-          for (int mm = 0; mm < G; ++mm) {
-            s0 += dword2(sm.gw[4 * mm], sm.gw[4 * mm + 1]);
-            s1 += dword2(sm.gw[4 * mm + 2], sm.gw[4 * mm + 3]);
-          }
-          gn_moments(s0, s1, (double)HID * T, 1e-8f, fmu, frs);
+          const double2 acc = member_sums2(sm.gw, G, lane);  // every member's GN2 sums, member order
+          gn_moments(acc.x, acc.y, (double)HID * T, 1e-8f, fmu, frs);
         }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
         float rsum = 0.f;
@@ -603,6 +614,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(9);
       // ---- residual update (model/model.py:345-352) ----
       const float afm = tf ? sm.af[m] : 1.f;
+      float kc[4] = {0.f, 0.f, 0.f, 0.f};  // this channel's residual-LN affines (GN_a: 0, 1; GN_b: 2, 3)
       if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
         // moment record of u = o + r' (r' = r a_f a_t), see device_common.h recursive_affine
         const float ga = LM == LD_RECURSIVE ? pm[PB_LNAG + m] : 0.f, be = LM == LD_RECURSIVE ? pm[PB_LNAB + m] : 0.f;
@@ -635,27 +647,31 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (k < 2 * NMOM * G) sm.gw[k] = v[0];
         }
       TPROBE(11);
-        __syncthreads();
-        if (tid < NMOM) {
-          double s = 0.0;
-          for (int mm = 0; mm < G; ++mm) s += dword2(sm.gw[2 * NMOM * mm + 2 * tid], sm.gw[2 * NMOM * mm + 2 * tid + 1]);
-          sm.dred[tid] = s;
+        __syncthreads();  // every member's moment words in LDS
+        // GN_a / GN_b of this thread's channel m, in-thread (member order as before: no LDS round trip of
+        // the sums or the affines, one barrier)
+        // lane j < NMOM of every wave sums moment j over the members (one LDS load per member per wave),
+        // then the 11 sums become wave-uniform by readlane
+        const double* gd = reinterpret_cast<const double*>(sm.gw);
+        double sj = 0.0;
+        {
+          const int j = lane < NMOM ? lane : 0;
+          for (int mm = 0; mm < G; ++mm) sj += gd[NMOM * mm + j];
         }
-        __syncthreads();
+        double ms[NMOM];
+#pragma unroll
+        for (int j = 0; j < NMOM; ++j) ms[j] = readlane_d(sj, j);
         if constexpr (LM == LD_RECURSIVE) {
           float mua, rsa, mub, rsb;
-          recursive_moments(sm.dred, reinterpret_cast<const double*>(pm + PB_WSUM), 1e-5f, 1e-5f, CH, T, mua, rsa,
-                            mub, rsb);
-          if (tid < CH) {  // as recursive_affine, one channel per thread
-            const float sa = rsa * pm[PB_LNAG + tid];
-            sm.c[0][tid] = sa; sm.c[1][tid] = pm[PB_LNAB + tid] - sa * mua;
-            const float sb = rsb * pm[PB_LNBG + tid];
-            sm.c[2][tid] = sb; sm.c[3][tid] = pm[PB_LNBB + tid] - sb * mub;
-          }
+          recursive_moments(ms, reinterpret_cast<const double*>(pm + PB_WSUM), 1e-5f, 1e-5f, CH, T, mua, rsa, mub,
+                            rsb);
+          kc[0] = rsa * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mua;  // as recursive_affine
+          kc[2] = rsb * pm[PB_LNBG + m]; kc[3] = pm[PB_LNBB + m] - kc[2] * mub;
         } else {
-          gn_affine_ch(tid, sm.dred + 2, T, 1e-5f, pm + PB_LNAG, pm + PB_LNAB, sm.c[0], sm.c[1]);
+          float mu, rs;
+          gn_moments(ms[2], ms[3], (double)CH * T, 1e-5f, mu, rs);  // as gn_affine
+          kc[0] = rs * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mu;
         }
-        __syncthreads();
       }
       // next block's conv1d weights: in flight during the x' update
       if (bi + 1 < a.nblk) {
@@ -667,7 +683,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int tl = trow(r);
         const float gte = tf ? afm * sm.at[tl] : 1.f;
-        const float x = resid_apply<LM>(o[r], rv[r], gte, m, sm.c[0], sm.c[1], sm.c[2], sm.c[3]);
+        const float x = resid_apply<LM>(o[r], rv[r], gte, 0, kc, kc + 1, kc + 2, kc + 3);
         o[r] = (t0 + tl < T) ? x : 0.f;
         split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
       }
