@@ -160,6 +160,9 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + PD) * 1024, 0);
       rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + PD) * 1024, 0);
     }
+    // keep program order per step: the scheduler otherwise may sink the refill loads to their use and
+    // collapse the ring to one step in flight (seen as s_waitcnt vmcnt(1) before every step)
+    __builtin_amdgcn_sched_barrier(0);
   };
 #pragma unroll
   for (int s0 = 0; s0 < NS - PD; s0 += PD) {
@@ -298,6 +301,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
   bool l2;
   {
+    if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact
+      if (tid < CH) sm.af[tid] = 1.f;
+      if (tid < FR) sm.at[tid] = 1.f;
+    }
     const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
     if (tid == 0) gput(slot(g, 1), a.tag0 + 1, xcc, false);
     const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
@@ -454,7 +461,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sc = rs * pm[PB_G1 + c];
           sh = pm[PB_BE1 + c] - sc * mu;
         }
-      TPROBE(13);
         float wv[2][4];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -501,7 +507,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           case 3: rows(std::integral_constant<int, 3>{}); break;
           default: rows(std::integral_constant<int, 4>{}); break;
         }
-      TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
       }
@@ -532,19 +537,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           gn_moments(acc.x, acc.y, (double)HID * T, 1e-8f, fmu, frs);
         }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
-        float rsum = 0.f;
+        float rsum = 0.f, csr[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int tl = trow(r);
           rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
-          const bool valid = t0 + tl < T;
-          if (valid) rsum += rv[r];
-          if (tf) {  // this frame's sum over the wave's 32 channels (lane 31: half 0 rows, lane 63: half 1)
-            const float cs = half_total(valid ? rv[r] : 0.f);
-            if ((lane & 31) == 31) sm.cs[tl][wave] = cs;
-          }
+          const float rm = t0 + tl < T ? rv[r] : 0.f;
+          rsum += rm;
+          csr[r] = half_total(rm);  // this frame's sum over the wave's 32 channels (lanes 31 / 63)
         }
-        if (tf) {  // P3 words: per-channel sums over own frames (a_f)
+        if (tf) {
+          if ((lane & 31) == 31) {  // one branch for the 16 frame sums
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm.cs[trow(r)][wave] = csr[r];
+          }
+          // P3 words: per-channel sums over own frames (a_f)
           rsum += __shfl_xor(rsum, 32);
           if (hl == 0) gputf(slot(g, e3) + GW_ROW + m, tag3, rsum, l2);
         }
@@ -613,7 +620,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       TPROBE(9);
       // ---- residual update (model/model.py:345-352) ----
-      const float afm = tf ? sm.af[m] : 1.f;
+      // gate r in place once: r' = r a_f a_t (a_f = a_t = 1 without TF-attention, set at kernel start)
+      {
+        const float afm = sm.af[m];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rv[r] = rv[r] * (afm * sm.at[trow(r)]);
+      }
       float kc[4] = {0.f, 0.f, 0.f, 0.f};  // this channel's residual-LN affines (GN_a: 0, 1; GN_b: 2, 3)
       if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
         // moment record of u = o + r' (r' = r a_f a_t), see device_common.h recursive_affine
@@ -625,7 +637,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         for (int r = 0; r < 16; ++r) {
           const int tl = trow(r);
           const float vm = (t0 + tl < T) ? 1.f : 0.f;  // masked, not branched
-          const float rp = vm * (tf ? rv[r] * (afm * sm.at[tl]) : rv[r]);
+          const float rp = vm * rv[r];
           if constexpr (LM == LD_RECURSIVE) {
             const float ov = vm * o[r], uv = ov + rp;
             mo[0] += ov; mo[1] += ov * ov; mo[2] += uv; mo[3] += uv * uv; mo[4] += be * ov; mo[5] += ga * uv;
@@ -672,18 +684,19 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           gn_moments(ms[2], ms[3], (double)CH * T, 1e-5f, mu, rs);  // as gn_affine
           kc[0] = rs * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mu;
         }
+      TPROBE(13);
       }
       // next block's conv1d weights: in flight during the x' update
       if (bi + 1 < a.nblk) {
         const __half* wn = wb + WF_BLOCK;
         prefetch_w(rsrc_of(wn), rsrc_of(wn + WF_W1L), voff1, rh, rl);
       }
+      TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int tl = trow(r);
-        const float gte = tf ? afm * sm.at[tl] : 1.f;
-        const float x = resid_apply<LM>(o[r], rv[r], gte, 0, kc, kc + 1, kc + 2, kc + 3);
+        const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
         o[r] = (t0 + tl < T) ? x : 0.f;
         split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
       }
