@@ -148,9 +148,15 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
                                           u32x4v (&rh)[PD], u32x4v (&rl)[PD], int lane) {
   static_assert(NS % PD == 0 && NS > PD, "K steps");
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
+  // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
+  f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff);
+  f16x8 al = *reinterpret_cast<const f16x8*>(Alo + aoff);
   auto step = [&](int s, int i, bool pf) {
-    const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * s);
-    const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * s);
+    f16x8 nh = ah, nl = al;
+    if (s + 1 < NS) {
+      nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
+      nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
+    }
     const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
     const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
@@ -160,6 +166,11 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + PD) * 1024, 0);
       rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + PD) * 1024, 0);
     }
+    ah = nh; al = nl;
+    // pipeline shape of a step: next step's A reads (DS), this step's 3 MFMAs, then the ring refill (VMEM)
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
     // keep program order per step: the scheduler otherwise may sink the refill loads to their use and
     // collapse the ring to one step in flight (seen as s_waitcnt vmcnt(1) before every step)
     __builtin_amdgcn_sched_barrier(0);
@@ -299,24 +310,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   unsigned ep = 1;  // epochs published so far (identical sequence in every member); epoch 1 = XCD ids
   // epoch 1: the members' XCD ids (write-through); if the whole group shares one XCD, every later
   // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
-  bool l2;
-  {
-    if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact
-      if (tid < CH) sm.af[tid] = 1.f;
-      if (tid < FR) sm.at[tid] = 1.f;
-    }
-    const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
-    if (tid == 0) gput(slot(g, 1), a.tag0 + 1, xcc, false);
-    const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
-    unsigned v[1];
-    gpoll<1>(p, a.tag0 + 1, v, a.err);
-    if (tid < G) sm.gw[tid] = v[0];
-    __syncthreads();
-    bool same = a.xmode == 0;
-    for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
-    l2 = same;
-    __syncthreads();
+  if (a.probe != nullptr && tid == 0) {  // entry: wall clock, and the shader clock (s_memtime) when nblk > 5
+    a.probe[(size_t)blockIdx.x * a.nblk * 16 + 15] = wall_clock64();
+    if (a.nblk > 5) a.probe[((size_t)blockIdx.x * a.nblk + 3) * 16 + 15] = __builtin_amdgcn_s_memtime();
   }
+  if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact
+    if (tid < CH) sm.af[tid] = 1.f;
+    if (tid < FR) sm.at[tid] = 1.f;
+  }
+  bool l2 = false;
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const int m = 32 * wave + (lane & 31);            // this lane's output channel in both GEMMs
   const int hl = lane >> 5;
@@ -326,35 +328,71 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const int voff1 = (wave * NS1 * 64 + lane) * 16, voff2 = (wave * NS2 * 64 + lane) * 16;
 
   for (int u = grp; u < a.B; u += ngroups) {
-    // ---- TCN input: x'_0 = TCN.LN(S0) (model/model.py:333), own frames, into o and the LDS A operand
+    // opaque per-utterance copies (as in the block loop): keeps hipcc from hoisting and spilling the
+    // per-row addresses of the prologue (their reloads waited on vmcnt(0) one by one)
+    int hl4u = 4 * hl, mu_ = m, tidu = tid;
+    asm volatile("" : "+v"(hl4u), "+v"(mu_), "+v"(tidu));
+    // ---- TCN input: x'_0 = TCN.LN(S0) (model/model.py:333), own frames, into o and the LDS A operand.
+    // The first-touch loads of the input (S0 rows, LN parameters, the LN records) are issued before
+    // anything waits, so their latencies overlap.
     float o[16];
+    u32x4v rh[PD], rl[PD];
     {
-      float pg[2], pb[2];
-      ld_chan(a.ln.g, CH, pg);
-      ld_chan(a.ln.be, CH, pb);
-      float raw[16];
-      const float* S0u = a.S0 + ((size_t)u * Tp + t0) * CH;
+    const int m = mu_, tid = tidu;
+    auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4u; };
+    float raw[16], pg[2], pb[2];
+    {
+      // buffer loads off one lane offset, the row as a constant offset (flat loads here got a fresh address
+      // pair per row and were serialized by s_waitcnt vmcnt(0) on register reuse, ~1.5 us each). All
+      // descriptors first, then one batch of loads (the sched barrier keeps descriptor set-up, which may
+      // reload spilled pointers and wait, from landing between the loads).
+      const __amdgpu_buffer_rsrc_t s0r = rsrc_of(a.S0 + ((size_t)u * Tp + t0) * CH);
+      const __amdgpu_buffer_rsrc_t gr = rsrc_of(a.ln.g), ber = rsrc_of(a.ln.be);
+      const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = t0 + trow(r);
-        raw[r] = t < T ? S0u[trow(r) * CH + m] : 0.f;
-      }
-      reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
+      for (int r = 0; r < 16; ++r)  // rows < G*32 <= Tp: in bounds (masked below)
+        raw[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s0r, vo, ((r & 3) + 8 * (r >> 2)) * CH * 4, 0));
+      // LN parameters of channel tid (threads tid < CH use them in gn_affine)
+      pg[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, co, 0, 0));
+      pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
+      pg[1] = pb[1] = 0.f;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
+    if (u == grp) {
+      // the members' XCD ids (write-through, epoch 1); if the whole group shares one XCD, every later
+      // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
+      const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
+      if (tid == 0) gput(slot(g, 1), a.tag0 + 1, xcc, false);
+      const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
+      unsigned v[1];
+      gpoll<1>(p, a.tag0 + 1, v, a.err);
+      if (tid < G) sm.gw[tid] = v[0];
       __syncthreads();
-      gn_affine(sm.dred, CH, T, a.ln.eps, pg, pb, sm.c[0], sm.c[1]);
-      __syncthreads();
+      bool same = a.xmode == 0;
+      for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
+      l2 = same;
+      if (a.probe != nullptr && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
+    }
+    __syncthreads();  // LN record sums (sm.dred) complete
+    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 2) a.probe[((size_t)blockIdx.x * a.nblk + 2) * 16 + 15] = wall_clock64();
+    gn_affine(sm.dred, CH, T, a.ln.eps, pg, pb, sm.c[0], sm.c[1]);
+    __syncthreads();
+    {
       const float s = sm.c[0][m], h = sm.c[1][m];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int tl = trow(r);
-        o[r] = (t0 + tl < T) ? fmaf(raw[r], s, h) : 0.f;
+        o[r] = fmaf(raw[r], s, h) * (t0 + tl < T ? 1.f : 0.f);
         split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
       }
     }
-    u32x4v rh[PD], rl[PD];
+    // block-0 conv1d weights last: every wait of the prologue (spill reloads wait on vmcnt(0)) is behind us
     prefetch_w(rsrc_of(a.wfrag), rsrc_of(a.wfrag + WF_W1L), voff1, rh, rl);
     __syncthreads();
 
+    }
     for (int bi = 0; bi < a.nblk; ++bi) {
       // Opaque per-iteration copies of the lane's row offset and channel: every per-row LDS address is then
       // base + immediate offset. Without this hipcc hoists the 16 row addresses of each array out of the
@@ -364,6 +402,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int m = mo_, tid = tido, lane = tid & 63;
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
+      if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
+        a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
       const __half* wb = a.wfrag + (size_t)bi * WF_BLOCK;
       const int li = bi % a.layer;
       const int dil = li == 0 ? 1 : (li % 4 + 1);   // model/model.py:285-295 (as api.hip packs it)
@@ -723,7 +763,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 }
 
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
-  if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || grid < a.G || grid % a.G) return hipErrorInvalidValue;
+  if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || grid < a.G || grid % a.G)
+    return hipErrorInvalidValue;
   switch (a.ln_mode) {
     case LD_RECURSIVE: hipLaunchKernelGGL(k_tcn<LD_RECURSIVE>, dim3(grid), dim3(NTHR), 0, s, a); break;
     case LD_RESIDUAL: hipLaunchKernelGGL(k_tcn<LD_RESIDUAL>, dim3(grid), dim3(NTHR), 0, s, a); break;

@@ -9,9 +9,9 @@ import numpy as np
 
 NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN2 stats", "res_out GEMM",
          "P2 wait", "rowsum/colsum", "P3 publish+wait", "gates", "moments", "P4 publish+wait", "x' update"]
-# sub-phase stamps currently placed in fused.hip: slot 13 after the GN1 affine (dwconv phase start),
-# slot 14 after the depthwise loop (before the GN2 block sums)
-SUB = [(13, 3, "dwconv: GN1 affine"), (14, 13, "dwconv: loop"), (4, 14, "dwconv: GN2 sums")]
+# sub-phase stamps currently placed in fused.hip: slot 13 after the residual-LN affines (x' update
+# phase start), slot 14 after the next block's weight prefetch is issued
+SUB = [(13, 11, "x': moments->affines"), (14, 13, "x': prefetch issue"), (12, 14, "x': update+barrier")]
 
 
 def main(path):
@@ -25,6 +25,20 @@ def main(path):
     blk = (st[:, :, 12] - st[:, :, 0])
     print(f"per block (median over workgroups): {np.median(blk):.2f} us; first block start spread "
           f"{st[:, 0, 0].max() - st[:, 0, 0].min():.2f} us; launch span {st[:, -1, 12].max() - st[:, 0, 0].min():.1f} us")
+    ent = full[:, 0, 15]
+    if (ent > 0).all():
+        print(f"kernel entry spread {ent.max() - ent.min():.2f} us; entry -> block 0 start: median "
+              f"{np.median(st[:, 0, 0] - ent):.2f} max {(st[:, 0, 0] - ent).max():.2f} us")
+        if nblk > 2 and (full[:, 1, 15] > 0).all() and (full[:, 2, 15] > 0).all():
+            x1, x2 = full[:, 1, 15], full[:, 2, 15]  # after the XCD exchange; after the input statistics
+            print(f"  prologue: first-touch loads + XCD exchange {np.median(x1 - ent):.2f}, record sums "
+                  f"{np.median(x2 - x1):.2f}, input LN {np.median(st[:, 0, 0] - x2):.2f} us (medians)")
+    if nblk > 5 and (full[:, 3:6, 15] > 0).all() and (ent > 0).all():
+        c3, c4, c5 = (full[:, k, 15] * 100.0 for k in (3, 4, 5))  # s_memtime ticks (undo the /100)
+        wp = st[:, 0, 0] - ent
+        wb = st[:, 2, 0] - st[:, 0, 0]
+        print(f"shader clock: prologue {np.median((c4 - c3) / wp) / 1e3:.2f} GHz, blocks 0-1 "
+              f"{np.median((c5 - c4) / wb) / 1e3:.2f} GHz")
     for i, n in enumerate(NAMES):
         v = d[:, 1:, i]  # skip block 0 (cold)
         print(f"  {n:24s} median {np.median(v):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
