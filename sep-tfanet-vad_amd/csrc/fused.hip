@@ -348,6 +348,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // reload spilled pointers and wait, from landing between the loads).
       const __amdgpu_buffer_rsrc_t s0r = rsrc_of(a.S0 + ((size_t)u * Tp + t0) * CH);
       const __amdgpu_buffer_rsrc_t gr = rsrc_of(a.ln.g), ber = rsrc_of(a.ln.be);
+      const __amdgpu_buffer_rsrc_t w1h = rsrc_of(a.wfrag), w1l = rsrc_of(a.wfrag + WF_W1L);
       const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -357,6 +358,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pg[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, co, 0, 0));
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
+      prefetch_w(w1h, w1l, voff1, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
     reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
@@ -388,8 +390,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
       }
     }
-    // block-0 conv1d weights last: every wait of the prologue (spill reloads wait on vmcnt(0)) is behind us
-    prefetch_w(rsrc_of(a.wfrag), rsrc_of(a.wfrag + WF_W1L), voff1, rh, rl);
     __syncthreads();
 
     }
