@@ -52,75 +52,105 @@ __device__ __forceinline__ void fft_stage(const float2* in, float2* out, const f
   out[idxD + 3 * Ns] = csub(a1, a3);
 }
 
-// 256-point transform ping-ponging between b0 and b1 (4 stages: result back in b0). Block-wide
-// barriers between stages (every wave of the block runs the same number of stages).
+// Orders this wave's LDS writes before its later LDS reads (the buffers of a transform belong to one
+// wave: no workgroup barrier is needed between its stages).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// 256-point transform of one wave ping-ponging between its buffers b0 and b1 (4 stages: result back
+// in b0); the caller's buffers must be complete for this wave (wave_lds_sync or a barrier) on entry.
 template <bool INV>
 __device__ inline void fft256(float2* b0, float2* b1, const float2* tw, int lane) {
   fft_stage<INV>(b0, b1, tw, lane, 1);
-  __syncthreads();
+  wave_lds_sync();
   fft_stage<INV>(b1, b0, tw, lane, 4);
-  __syncthreads();
+  wave_lds_sync();
   fft_stage<INV>(b0, b1, tw, lane, 16);
-  __syncthreads();
+  wave_lds_sync();
   fft_stage<INV>(b1, b0, tw, lane, 64);
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
   __shared__ float2 tw[512];
   __shared__ float2 work[4][2][M256];
+  __shared__ float2 xt[FR_PER_WG][NBIN + 1];   // this block's frames, for the bin-major side outputs
+  __shared__ float dt[FR_PER_WG][NBIN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x, f0 = blockIdx.y * FR_PER_WG;
   for (int i = tid; i < 512; i += 256) tw[i] = a.tw[i];
   const float* xb = a.x + (size_t)b * a.ldx;
   const int N = a.N;
-  for (int round = 0; round < FR_PER_WG / 4; ++round) {
-    const int f = f0 + round * 4 + wave;
+  constexpr int NR = FR_PER_WG / 4;
+  // all of this wave's input samples first (frames f0 + 4 round + wave), so the loads of the four
+  // transforms are in flight together; frames >= T load frame T-1's (in bounds, unused)
+  float2 z[NR][4];
+#pragma unroll
+  for (int round = 0; round < NR; ++round) {
+    const int f = min(f0 + round * 4 + wave, a.T - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = lane + 64 * r;
+      int s0 = f * HOP + 2 * m - HOP, s1 = s0 + 1;  // reflect padding of 256 on both sides
+      s0 = s0 < 0 ? -s0 : (s0 >= N ? 2 * (N - 1) - s0 : s0);
+      s1 = s1 < 0 ? -s1 : (s1 >= N ? 2 * (N - 1) - s1 : s1);
+      z[round][r] = make_float2(xb[s0], xb[s1]);
+    }
+  }
+  __syncthreads();  // twiddles
+  const bool side = a.Xout != nullptr || a.spec_out != nullptr;
+#pragma unroll
+  for (int round = 0; round < NR; ++round) {
+    const int fi = round * 4 + wave, f = f0 + fi;
     const bool live = f < a.T;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = lane + 64 * r;
-      float2 z = make_float2(0.f, 0.f);
-      if (live) {
-        int s0 = f * HOP + 2 * m - HOP, s1 = s0 + 1;  // reflect padding of 256 on both sides
-        s0 = s0 < 0 ? -s0 : (s0 >= N ? 2 * (N - 1) - s0 : s0);
-        s1 = s1 < 0 ? -s1 : (s1 >= N ? 2 * (N - 1) - s1 : s1);
-        z = make_float2(a.window[2 * m] * xb[s0], a.window[2 * m + 1] * xb[s1]);
-      }
-      work[wave][0][m] = z;
+      work[wave][0][m] = make_float2(a.window[2 * m] * z[round][r].x, a.window[2 * m + 1] * z[round][r].y);
     }
-    __syncthreads();
+    wave_lds_sync();
     fft256<false>(work[wave][0], work[wave][1], tw, lane);
-    if (live) {
-      const float2* Z = work[wave][0];
-      const size_t row = (size_t)b * a.Tp + f;
+    const float2* Z = work[wave][0];
+    const size_t row = (size_t)b * a.Tp + f;
 #pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const int k = lane + 64 * r;
-        if (k > 256) break;
-        float2 Xk;
-        if (k == 256) {
-          Xk = make_float2(Z[0].x - Z[0].y, 0.f);       // Nyquist: E[0] - O[0]
-        } else {
-          const float2 zk = Z[k], zm = conjf2(Z[(M256 - k) & 255]);
-          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
-          const float2 Dd = csub(zk, zm);
-          const float2 O = make_float2(0.5f * Dd.y, -0.5f * Dd.x);
-          Xk = cadd(E, cmul(tw[k], O));
-        }
-        if (k == 0) Xk = make_float2(0.f, 0.f);       // DC removed (model/model.py:24,410)
-        if (a.X) a.X[row * NBIN + k] = Xk;
-        if (a.Xout) a.Xout[((size_t)b * NBIN + k) * a.T + f] = Xk;
-        if (a.specdb || a.spec_out) {
-          const float mag = hypotf(Xk.x, Xk.y);   // torch.abs(complex)
-          const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
-          if (a.specdb) a.specdb[row * SPEC_LD + k] = db;
-          if (a.spec_out) a.spec_out[((size_t)b * NBIN + k) * a.T + f] = db;
-        }
+    for (int r = 0; r < 5; ++r) {
+      const int k = lane + 64 * r;
+      if (k > 256) break;
+      float2 Xk;
+      if (k == 256) {
+        Xk = make_float2(Z[0].x - Z[0].y, 0.f);       // Nyquist: E[0] - O[0]
+      } else {
+        const float2 zk = Z[k], zm = conjf2(Z[(M256 - k) & 255]);
+        const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
+        const float2 Dd = csub(zk, zm);
+        const float2 O = make_float2(0.5f * Dd.y, -0.5f * Dd.x);
+        Xk = cadd(E, cmul(tw[k], O));
       }
+      if (k == 0) Xk = make_float2(0.f, 0.f);       // DC removed (model/model.py:24,410)
+      const float mag = hypotf(Xk.x, Xk.y);         // torch.abs(complex)
+      const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
+      if (live) {
+        if (a.X) a.X[row * NBIN + k] = Xk;
+        if (a.specdb) a.specdb[row * SPEC_LD + k] = db;
+      }
+      if (side) { xt[fi][k] = Xk; dt[fi][k] = db; }
     }
+    wave_lds_sync();  // this wave's next round overwrites work[wave]
+  }
+  // bin-major side outputs [B][NBIN][T]: runs of FR_PER_WG consecutive frames per bin
+  if (side) {
     __syncthreads();
+    const int nf = min(FR_PER_WG, a.T - f0);
+    for (int i = tid; i < NBIN * FR_PER_WG; i += 256) {
+      const int k = i / FR_PER_WG, fi = i % FR_PER_WG;
+      if (fi >= nf) continue;
+      const size_t o = ((size_t)b * NBIN + k) * a.T + f0 + fi;
+      if (a.Xout) a.Xout[o] = xt[fi][k];
+      if (a.spec_out) a.spec_out[o] = dt[fi][k];
+    }
   }
 }
 
@@ -214,16 +244,41 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   const int fbeg = f0 - 1;
   for (int i = tid; i < 512; i += 512) { tw[i] = a.tw[i]; win[i] = a.window[i]; }
 
+  // Every input load of the block is issued up front (forward mode): the X / mask rows of the computed
+  // frames into registers, the VAD features, then the BN_1 records. The block then waits once instead
+  // of three dependent HBM round trips (records -> features -> rows). Frames outside [0, T) load a
+  // clamped in-bounds row and are masked to zero on use.
+  constexpr int NE = (IS_FR * NBIN + 511) / 512;
+  float2 xr[NE];
+  float mr[NE];
+  float yv = 0.f;
+  const bool fwd = a.est_mode != 0;
+  const bool vad = fwd && a.has_vad;
+  if (fwd) {
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int i = min(tid + j * 512, IS_FR * NBIN - 1);
+      const int fi = i / NBIN, k = i - fi * NBIN;
+      const int fc = min(max(fbeg + fi, 0), T - 1);
+      const size_t row = (size_t)b * a.Tp + fc;
+      xr[j] = a.X[row * NBIN + k];
+      mr[j] = a.masks[row * MOUT_PAD + s * NBIN + k];
+    }
+    if (vad && tid < 4 * (IS_FR + 6)) {
+      const int o = tid / (IS_FR + 6), q = tid % (IS_FR + 6);
+      const int fc = min(max(fbeg - 3 + q, 0), T - 1);
+      yv = a.vy[((size_t)bs * 4 + o) * a.Tp + fc];
+    }
+  }
+
   // 0) VAD tail for the frames this block needs
-  if (a.est_mode && a.has_vad) {
+  if (vad) {
     gn_from_records(a.vgn, bs, 4, T, vs, vh, dacc);  // BN_1 = GroupNorm(1, 4, eps 1e-8)
     __syncthreads();
     if (tid < 4 * (IS_FR + 6)) {
       const int o = tid / (IS_FR + 6), q = tid % (IS_FR + 6);
       const int f = fbeg - 3 + q;
-      float v = 0.f;
-      if (f >= 0 && f < T) v = fmaf(a.vy[((size_t)bs * 4 + o) * a.Tp + f], vs[o], vh[o]);
-      yn[o][q] = v;
+      yn[o][q] = (f >= 0 && f < T) ? fmaf(yv, vs[o], vh[o]) : 0.f;
     }
     __syncthreads();
     if (tid < IS_FR + 4) {
@@ -260,25 +315,30 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   __syncthreads();
 
   // 1) est for the computed frames (frame-major, coalesced over bins)
-  for (int i = tid; i < IS_FR * NBIN; i += 512) {
-    const int fi = i / NBIN, k = i % NBIN;
-    const int f = fbeg + fi;
-    float2 e = make_float2(0.f, 0.f);
-    float m = 0.f;
-    if (f >= 0 && f < T) {
-      if (a.est_mode) {
-        const size_t row = (size_t)b * a.Tp + f;
-        const float2 X = a.X[row * NBIN + k];
-        m = sigmoid_f(a.masks[row * MOUT_PAD + s * NBIN + k]);
+  if (fwd) {
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int i = tid + j * 512;
+      if (i < IS_FR * NBIN) {
+        const int fi = i / NBIN, k = i - fi * NBIN;
+        const int f = fbeg + fi;
+        const bool ok = f >= 0 && f < T;
         // noisy-phase synthesis (|X| m) e^{j angle X} == X m up to rounding (model/model.py:430-437)
+        const float m = ok ? sigmoid_f(mr[j]) : 0.f;
         const float g = gain[fi];
-        e = make_float2(g * (X.x * m), g * (X.y * m));
-      } else {
-        e = a.est_in[((size_t)bs * NBIN + k) * T + f];
+        spec[fi][k] = ok ? make_float2(g * (xr[j].x * m), g * (xr[j].y * m)) : make_float2(0.f, 0.f);
+        mk[fi][k] = m;
       }
     }
-    spec[fi][k] = e;
-    mk[fi][k] = m;
+  } else {
+    for (int i = tid; i < IS_FR * NBIN; i += 512) {
+      const int fi = i / NBIN, k = i % NBIN;
+      const int f = fbeg + fi;
+      float2 e = make_float2(0.f, 0.f);
+      if (f >= 0 && f < T) e = a.est_in[((size_t)bs * NBIN + k) * T + f];
+      spec[fi][k] = e;
+      mk[fi][k] = 0.f;
+    }
   }
   __syncthreads();
   // side outputs of the owned frames, bin-major [bs][k][f] (15 consecutive frames per bin)
@@ -292,7 +352,9 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       if (a.mask_out) a.mask_out[o] = mk[fo + 1][k];
     }
   }
-  // 2) inverse real FFT per frame: 8 waves x 2 rounds = 16 frames
+  __syncthreads();  // side outputs read spec rows that the transforms below overwrite
+  // 2) inverse real FFT per frame: 8 waves x 2 rounds = 16 frames, each wave on its own rows (wave-local
+  // ordering only)
   for (int round = 0; round < IS_FR / 8; ++round) {
     const int fi = round * 8 + wave;
     float2* Y = spec[fi];
@@ -310,7 +372,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       const float2 Oo = cmul(make_float2(0.5f * Dd.x, 0.5f * Dd.y), w);
       w0[k] = make_float2(E.x - Oo.y, E.y + Oo.x);  // E + i O
     }
-    __syncthreads();
+    wave_lds_sync();
     // ping-pong with the (now consumed) spec row of this frame; result lands in w0
     fft256<true>(w0, Y, tw, lane);
     float* fr = reinterpret_cast<float*>(Y);  // time samples overwrite the frame's spectrum row
@@ -322,8 +384,9 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       fr[2 * m] = v.x * sc * win[2 * m];
       fr[2 * m + 1] = v.y * sc * win[2 * m + 1];
     }
-    __syncthreads();
+    wave_lds_sync();
   }
+  __syncthreads();  // every frame's time samples in place for the overlap-add
   // 3) overlap-add of the owned segments, divided by the window envelope (torch.istft)
   const int nseg = min(IS_OWN, T - f0) + ((f0 + IS_OWN >= T) ? 1 : 0);
   float* yb = a.y + (size_t)bs * a.N;
