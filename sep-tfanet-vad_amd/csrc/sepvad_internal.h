@@ -144,7 +144,7 @@ struct StftArgs {
   float* spec_out;       // nullable [B][NBIN][T] (debug entry)
 };
 
-constexpr int VAD_ROWS = 16;
+constexpr int VAD_ROWS = 32;
 struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4) partial stats
   int B, T, Tp, masked_speakers;
   const float* masks;    // [B][Tp][MOUT_PAD] pre-sigmoid

@@ -162,52 +162,79 @@ hipError_t launch_stft(const StftArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// VAD conv1_1 for 16 frames of one (utterance, speaker): thread = (frame i, channel group g).
+// VAD conv1_1 for VAD_ROWS = 32 frames of one (utterance, speaker). Thread = input channel c (the
+// 257th channel is folded in after the lane reduction): the thread's 20 taps stay in registers, its
+// R + 4 input samples (one coalesced 1 KB row read per frame, every load in flight at once) form a
+// register window, and it accumulates all R x 4 outputs. The 128 partial outputs are reduced over
+// the wave by recursive halving (lane L ends with outputs 2L, 2L+1: 126 lane exchanges), then over
+// the 4 waves through LDS in fixed order (deterministic).
+__device__ __forceinline__ float vad_in(const Vad1Args& a, int b, int s, int t, int c) {
+  const int tc = min(max(t, 0), a.T - 1);
+  const size_t row = (size_t)b * a.Tp + tc;
+  float v = a.masks[row * MOUT_PAD + s * NBIN + c];
+  if (a.masked_speakers) {
+    const float2 X = a.X[row * NBIN + c];
+    v = hypotf(X.x, X.y) * sigmoid_f(v);
+  }
+  return (t >= 0 && t < a.T) ? v : 0.f;  // conv zero padding (padding 2)
+}
+
 __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   constexpr int R = VAD_ROWS;
-  __shared__ float Mt[R + 4][NBIN + 1];   // input rows t0-2 .. t0+R+1
-  __shared__ float part[16][R][4];
+  constexpr int NV = 4 * R;   // outputs of the block, index 4 i + o
+  __shared__ float part[4][NV];
   __shared__ float red[2 * 16];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bs = blockIdx.x, b = bs >> 1, s = bs & 1;
   const int t0 = blockIdx.y * R;
   const int T = a.T;
-  for (int i = tid; i < (R + 4) * NBIN; i += 256) {
-    const int rr = i / NBIN, c = i % NBIN;
-    const int t = t0 - 2 + rr;
-    float v = 0.f;
-    if (t >= 0 && t < T) {
-      v = a.masks[((size_t)b * a.Tp + t) * MOUT_PAD + s * NBIN + c];
-      if (a.masked_speakers) {
-        const float2 X = a.X[((size_t)b * a.Tp + t) * NBIN + c];
-        v = hypotf(X.x, X.y) * sigmoid_f(v);
-      }
+  float m[R + 4];
+#pragma unroll
+  for (int r = 0; r < R + 4; ++r) m[r] = vad_in(a, b, s, t0 - 2 + r, tid);
+  float w[4][5];
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[o][k] = a.w1[((size_t)o * NBIN + tid) * 5 + k];
+  float acc[NV];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) v = fmaf(w[o][k], m[i + k], v);
+      acc[4 * i + o] = v;
     }
-    Mt[rr][c] = v;
+  // recursive halving over the lanes: partner lane ^ msk; the lower lane keeps the lower half
+#pragma unroll
+  for (int msk = 32, n = NV; msk >= 1; msk >>= 1, n >>= 1) {
+    const bool hi = (lane & msk) != 0;
+#pragma unroll
+    for (int j = 0; j < n / 2; ++j) {
+      const float send = hi ? acc[j] : acc[j + n / 2];
+      const float keep = hi ? acc[j + n / 2] : acc[j];
+      acc[j] = keep + __shfl_xor(send, msk);
+    }
   }
-  __syncthreads();
-  const int i = tid & 15, g = tid >> 4;
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-  for (int c = g; c < NBIN; c += 16) {
-    const float* w0 = a.w1 + ((size_t)0 * NBIN + c) * 5;
-    const float* w1 = a.w1 + ((size_t)1 * NBIN + c) * 5;
-    const float* w2 = a.w1 + ((size_t)2 * NBIN + c) * 5;
-    const float* w3 = a.w1 + ((size_t)3 * NBIN + c) * 5;
+  // channel 256 (the Nyquist bin): lane L of wave 0 adds its contribution to outputs 2L, 2L+1
+  if (wave == 0) {
+    const int i = lane >> 1, o0 = 2 * (lane & 1);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const float x = Mt[i + k][c];
-      acc0 = fmaf(w0[k], x, acc0); acc1 = fmaf(w1[k], x, acc1);
-      acc2 = fmaf(w2[k], x, acc2); acc3 = fmaf(w3[k], x, acc3);
+      const float x = vad_in(a, b, s, t0 + i - 2 + k, NBIN - 1);
+      acc[0] = fmaf(a.w1[((size_t)o0 * NBIN + NBIN - 1) * 5 + k], x, acc[0]);
+      acc[1] = fmaf(a.w1[((size_t)(o0 + 1) * NBIN + NBIN - 1) * 5 + k], x, acc[1]);
     }
   }
-  part[g][i][0] = acc0; part[g][i][1] = acc1; part[g][i][2] = acc2; part[g][i][3] = acc3;
+  part[wave][2 * lane] = acc[0];
+  part[wave][2 * lane + 1] = acc[1];
   __syncthreads();
   float st[2] = {0.f, 0.f};
-  if (tid < 4 * R) {
+  if (tid < NV) {
     const int ii = tid >> 2, o = tid & 3;
     const int t = t0 + ii;
-    float y = 0.f;
-    for (int q = 0; q < 16; ++q) y += part[q][ii][o];
+    const float y = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
     const float v = prelu_f(y + a.b1[o], a.alpha);
     a.vy[(((size_t)b * 2 + s) * 4 + o) * a.Tp + t] = (t < T) ? v : 0.f;
     if (t < T) { st[0] = v; st[1] = v * v; }
