@@ -12,6 +12,16 @@ namespace sepvad {
 __device__ __forceinline__ float prelu_f(float x, float w) { return x > 0.f ? x : w * x; }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
+// Workgroup barrier that orders LDS only. __syncthreads() carries a workgroup-scope fence, which hipcc
+// lowers to s_waitcnt vmcnt(0) before s_barrier: every wave would first wait for all of its outstanding
+// global stores (e.g. side outputs) to complete. Kernels whose threads never read each other's global
+// writes within the launch synchronise with this instead.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Sum over the 64 lanes of a wave; callers use lane 0's value (fixed order => deterministic).
 template <typename Tv>
 __device__ __forceinline__ Tv wave_sum(Tv v) {
@@ -25,9 +35,9 @@ __device__ __forceinline__ Tv wave_sum(Tv v) {
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
+  lds_sync();
   if (l == 0) red[w] = v;
-  __syncthreads();
+  lds_sync();
   double s = 0.0;
   const int nw = blockDim.x >> 6;
   for (int i = 0; i < nw; ++i) s += red[i];
@@ -45,7 +55,7 @@ __device__ __forceinline__ void block_reduce_store(float (&v)[NV], float* lds, d
     const float s = wave_sum(v[j]);
     if (l == 0) lds[j * 16 + w] = s;
   }
-  __syncthreads();
+  lds_sync();
   if (threadIdx.x < NV) {
     double s = 0.0;
     for (int i = 0; i < nw; ++i) s += lds[threadIdx.x * 16 + i];
@@ -135,7 +145,7 @@ __device__ inline void block_reduce_store_lds(float (&v)[NV], float* lds, double
   const int pos = (t >> 4) * 17 + (t & 15);  // rows of 16 padded to 17: conflict-free row sums
 #pragma unroll
   for (int j = 0; j < NV; ++j) lds[j * 272 + pos] = v[j];
-  __syncthreads();
+  lds_sync();
   if (t < NV * 16) {
     const int j = t >> 4, part = t & 15;
     float s = 0.f;
@@ -143,7 +153,7 @@ __device__ inline void block_reduce_store_lds(float (&v)[NV], float* lds, double
     for (int u = 0; u < 16; ++u) s += lds[j * 272 + part * 17 + u];
     lds[NV * 272 + t] = s;
   }
-  __syncthreads();
+  lds_sync();
   if (t < NV) {
     double s = 0.0;
 #pragma unroll

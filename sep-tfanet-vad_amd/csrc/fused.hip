@@ -288,10 +288,31 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   }
 }
 
+// This thread's workgroup-relative id, recomputed where it is needed: the wave index from a wave-uniform
+// SGPR, the lane from v_mbcnt (volatile asm: never hoisted). Values derived from threadIdx.x before the
+// utterance loop stay live across all of it; at 256 VGPRs hipcc spills them to scratch, and the first
+// reloads of a launch (behind the scratch spill stores, vmcnt(0)) cost ~15 us of cold-start latency.
+__device__ __forceinline__ int fresh_tid(int wave_s) {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return wave_s * 64 + l;
+}
+
+// The kernel arguments re-read from the kernarg segment (scalar loads through an opaque pointer) where
+// the prologue uses them: pointers held in registers across the utterance loop end up in VGPRs and are
+// spilled to scratch at this register pressure.
+typedef const __attribute__((address_space(4))) TcnArgs* KArgs;
+__device__ __forceinline__ KArgs kargs() {
+  KArgs p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <int LM>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   __shared__ __attribute__((aligned(16))) TcnSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const int G = a.G;
   // block -> (group, member): members of a group on one XCD when the grid is a multiple of 8*G
   int grp, g;
@@ -330,8 +351,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   for (int u = grp; u < a.B; u += ngroups) {
     // opaque per-utterance copies (as in the block loop): keeps hipcc from hoisting and spilling the
     // per-row addresses of the prologue (their reloads waited on vmcnt(0) one by one)
-    int hl4u = 4 * hl, mu_ = m, tidu = tid;
-    asm volatile("" : "+v"(hl4u), "+v"(mu_), "+v"(tidu));
+    const int tidu = fresh_tid(wave_s);
+    const int hl4u = 4 * ((tidu >> 5) & 1), mu_ = 32 * wave_s + (tidu & 31);
     // ---- TCN input: x'_0 = TCN.LN(S0) (model/model.py:333), own frames, into o and the LDS A operand.
     // The first-touch loads of the input (S0 rows, LN parameters, the LN records) are issued before
     // anything waits, so their latencies overlap.
@@ -346,10 +367,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // pair per row and were serialized by s_waitcnt vmcnt(0) on register reuse, ~1.5 us each). All
       // descriptors first, then one batch of loads (the sched barrier keeps descriptor set-up, which may
       // reload spilled pointers and wait, from landing between the loads).
-      const __amdgpu_buffer_rsrc_t s0r = rsrc_of(a.S0 + ((size_t)u * Tp + t0) * CH);
-      const __amdgpu_buffer_rsrc_t gr = rsrc_of(a.ln.g), ber = rsrc_of(a.ln.be);
-      const __amdgpu_buffer_rsrc_t w1h = rsrc_of(a.wfrag), w1l = rsrc_of(a.wfrag + WF_W1L);
+      const KArgs ka = kargs();
+      const __amdgpu_buffer_rsrc_t s0r = rsrc_of(ka->S0 + ((size_t)u * Tp + t0) * CH);
+      const __amdgpu_buffer_rsrc_t gr = rsrc_of(ka->ln.g), ber = rsrc_of(ka->ln.be);
+      const __amdgpu_buffer_rsrc_t w1h = rsrc_of(ka->wfrag), w1l = rsrc_of(ka->wfrag + WF_W1L);
       const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
+      const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * 16;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 16; ++r)  // rows < G*32 <= Tp: in bounds (masked below)
@@ -358,10 +381,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pg[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, co, 0, 0));
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
-      prefetch_w(w1h, w1l, voff1, rh, rl);  // block-0 conv1d weights: in flight with the input rows
+      prefetch_w(w1h, w1l, voffu, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
     reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
+    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 7) * 16 + 15] = wall_clock64();
     if (u == grp) {
       // the members' XCD ids (write-through, epoch 1); if the whole group shares one XCD, every later
       // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
@@ -379,7 +404,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     }
     __syncthreads();  // LN record sums (sm.dred) complete
     if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 2) a.probe[((size_t)blockIdx.x * a.nblk + 2) * 16 + 15] = wall_clock64();
-    gn_affine(sm.dred, CH, T, a.ln.eps, pg, pb, sm.c[0], sm.c[1]);
+    {  // gn_affine with this iteration's thread id (channel tid < CH)
+      float mu, rs;
+      gn_moments(sm.dred[0], sm.dred[1], (double)CH * T, a.ln.eps, mu, rs);
+      if (tid < CH) {
+        const float sc = rs * pg[0];
+        sm.c[0][tid] = sc;
+        sm.c[1][tid] = pb[0] - sc * mu;
+      }
+    }
     __syncthreads();
     {
       const float s = sm.c[0][m], h = sm.c[1][m];
@@ -397,9 +430,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // Opaque per-iteration copies of the lane's row offset and channel: every per-row LDS address is then
       // base + immediate offset. Without this hipcc hoists the 16 row addresses of each array out of the
       // block loop as invariants, runs out of registers and spills them (scratch reloads on every row).
-      int hl4o = 4 * hl, mo_ = 32 * wave + (lane & 31), tido = threadIdx.x;
-      asm volatile("" : "+v"(hl4o), "+v"(mo_), "+v"(tido));
-      const int m = mo_, tid = tido, lane = tid & 63;
+      const int tido = fresh_tid(wave_s);
+      const int hl4o = 4 * ((tido >> 5) & 1), mo_ = 32 * wave_s + (tido & 31);
+      const int m = mo_, tid = tido, lane = tid & 63, hl = hl4o >> 2, wave = wave_s;
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
       if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
@@ -745,12 +778,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     }
     // ---- TCN output x' (head input) and the statistics of PReLU(x') for TCN.output.1 ----
     {
+      const int tidt = fresh_tid(wave_s);
+      const int hl4t = 4 * ((tidt >> 5) & 1), mt_ = 32 * wave_s + (tidt & 31);
+      auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4t; };
       float st[2] = {0.f, 0.f};
       float* Xu = a.Xfin + ((size_t)u * Tp + t0) * CH;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = t0 + trow(r);
-        if (t < Tp) Xu[trow(r) * CH + m] = o[r];
+        if (t < Tp) Xu[trow(r) * CH + mt_] = o[r];
         if (t < T) {
           const float pv = prelu_f(o[r], a.alpha_h);
           st[0] += pv; st[1] += pv * pv;

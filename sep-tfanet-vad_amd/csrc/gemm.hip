@@ -375,10 +375,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
     }
     if (a.Yside) {
       __syncthreads();
-      for (int i = tid; i < BMC * BT; i += 256) {
-        const int mm = m0 + i / BT, tl = i % BT;
-        const int t = t0 + tl;
-        if (mm < a.Mreal && t < T) a.Yside[((size_t)b * a.Mreal + mm) * T + t] = tr[(i / BT) * 65 + tl];
+      // all LDS reads first, then the stores (no per-element read -> wait -> store chain)
+      constexpr int NI = BMC * BT / 256;
+      float tv[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int i = tid + 256 * j;
+        tv[j] = tr[(i / BT) * 65 + i % BT];
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int i = tid + 256 * j;
+        const int mm = m0 + i / BT, t = t0 + i % BT;
+        if (mm < a.Mreal && t < T) a.Yside[((size_t)b * a.Mreal + mm) * T + t] = tv[j];
       }
     }
   }

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
       z[round][r] = make_float2(xb[s0], xb[s1]);
     }
   }
-  __syncthreads();  // twiddles
+  lds_sync();  // twiddles
   const bool side = a.Xout != nullptr || a.spec_out != nullptr;
 #pragma unroll
   for (int round = 0; round < NR; ++round) {
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
   }
   // bin-major side outputs [B][NBIN][T]: runs of FR_PER_WG consecutive frames per bin
   if (side) {
-    __syncthreads();
+    lds_sync();
     const int nf = min(FR_PER_WG, a.T - f0);
     for (int i = tid; i < NBIN * FR_PER_WG; i += 256) {
       const int k = i / FR_PER_WG, fi = i % FR_PER_WG;
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   }
   part[wave][2 * lane] = acc[0];
   part[wave][2 * lane + 1] = acc[1];
-  __syncthreads();
+  lds_sync();
   float st[2] = {0.f, 0.f};
   if (tid < NV) {
     const int ii = tid >> 2, o = tid & 3;
@@ -301,13 +301,13 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   // 0) VAD tail for the frames this block needs
   if (vad) {
     gn_from_records(a.vgn, bs, 4, T, vs, vh, dacc);  // BN_1 = GroupNorm(1, 4, eps 1e-8)
-    __syncthreads();
+    lds_sync();
     if (tid < 4 * (IS_FR + 6)) {
       const int o = tid / (IS_FR + 6), q = tid % (IS_FR + 6);
       const int f = fbeg - 3 + q;
       yn[o][q] = (f >= 0 && f < T) ? fmaf(yv, vs[o], vh[o]) : 0.f;
     }
-    __syncthreads();
+    lds_sync();
     if (tid < IS_FR + 4) {
       const int f = fbeg - 2 + tid;
       float z = a.b2;
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       vadv[tid] = (f >= 0 && f < T) ? p : 0.f;
       if (!a.kw_enabled && f >= f0 && f < f0 + IS_OWN && f < T) a.vad_out[(size_t)bs * T + f] = p;
     }
-    __syncthreads();
+    lds_sync();
     if (tid < IS_FR) {
       const int f = fbeg + tid;
       float g = 1.f;
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   } else {
     if (tid < IS_FR) gain[tid] = 1.f;
   }
-  __syncthreads();
+  lds_sync();
 
   // 1) est for the computed frames (frame-major, coalesced over bins)
   if (fwd) {
@@ -367,19 +367,33 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       mk[fi][k] = 0.f;
     }
   }
-  __syncthreads();
+  lds_sync();
   // side outputs of the owned frames, bin-major [bs][k][f] (15 consecutive frames per bin)
   if (a.est_mode && (a.est_out || a.mask_out)) {
-    for (int i = tid; i < NBIN * IS_OWN; i += 512) {
-      const int k = i / IS_OWN, fo = i % IS_OWN;
+    // all LDS reads first, then the stores (no per-element read -> wait -> store chain)
+    constexpr int NI = (NBIN * IS_OWN + 511) / 512;
+    float2 ev[NI];
+    float mv[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = min(tid + j * 512, NBIN * IS_OWN - 1);
+      const int k = i / IS_OWN, fo = i - k * IS_OWN;
+      ev[j] = spec[fo + 1][k];
+      mv[j] = mk[fo + 1][k];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = tid + j * 512;
+      const int k = i / IS_OWN, fo = i - k * IS_OWN;
       const int f = f0 + fo;
-      if (f >= T) continue;
-      const size_t o = ((size_t)bs * NBIN + k) * T + f;
-      if (a.est_out) a.est_out[o] = spec[fo + 1][k];
-      if (a.mask_out) a.mask_out[o] = mk[fo + 1][k];
+      if (i < NBIN * IS_OWN && f < T) {
+        const size_t o = ((size_t)bs * NBIN + k) * T + f;
+        if (a.est_out) a.est_out[o] = ev[j];
+        if (a.mask_out) a.mask_out[o] = mv[j];
+      }
     }
   }
-  __syncthreads();  // side outputs read spec rows that the transforms below overwrite
+  lds_sync();  // side outputs read spec rows that the transforms below overwrite
   // 2) inverse real FFT per frame: 8 waves x 2 rounds = 16 frames, each wave on its own rows (wave-local
   // ordering only)
   for (int round = 0; round < IS_FR / 8; ++round) {
@@ -413,7 +427,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
     }
     wave_lds_sync();
   }
-  __syncthreads();  // every frame's time samples in place for the overlap-add
+  lds_sync();  // every frame's time samples in place for the overlap-add
   // 3) overlap-add of the owned segments, divided by the window envelope (torch.istft)
   const int nseg = min(IS_OWN, T - f0) + ((f0 + IS_OWN >= T) ? 1 : 0);
   float* yb = a.y + (size_t)bs * a.N;

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
     if (t >= 0 && t < T && f >= 0 && f < NBIN) v = a.specdb[((size_t)b * a.Tp + t) * SPEC_LD + f];
     S[rr][ff] = v;
   }
-  __syncthreads();
+  lds_sync();
   float w[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) w[i] = a.w[i];
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
       }
       mC[c] = v;
     }
-    __syncthreads();
+    lds_sync();
     yf[c + 4] = p[11] + p[8] * mT[c + 3] + p[9] * mT[c + 4] + p[10] * mT[c + 5];
     if (c < R + 8) {
       const int t = t0 - 4 + c;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
       if (t >= 0 && t < T && c >= 1 && c < R + 7) v = p[3] + p[0] * mC[c - 1] + p[1] * mC[c] + p[2] * mC[c + 1];
       yt[c] = v;
     }
-    __syncthreads();
+    lds_sync();
     {
       const float v = p[15] + p[12] * yf[c + 2] + p[13] * yf[c + 4] + p[14] * yf[c + 6];
       afc = sigmoid_f(prelu_f(v, p[17]));
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_att_stats(AttStatsArgs a) {
       const float v = p[7] + p[4] * yt[k - 2] + p[5] * yt[k] + p[6] * yt[k + 2];
       ats[c] = sigmoid_f(prelu_f(v, p[16]));
     }
-    __syncthreads();
+    lds_sync();
     if (blockIdx.y == 0) a.af[(size_t)b * CH + c] = afc;
     if (c < R) a.at[(size_t)b * a.Tp + t0 + c] = ats[c];
   }
@@ -252,12 +252,12 @@ __global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
     float ga[2], ba[2], gb[2], bb[2];
     ld_chan(ld.gn.g, CH, ga); ld_chan(ld.gn.be, CH, ba); ld_chan(ld.g2, CH, gb); ld_chan(ld.be2, CH, bb);
     reduce_records(rec_src(ld.gn, b, NMOM), rec_none(), dacc);
-    __syncthreads();
+    lds_sync();
     recursive_affine(dacc, ld, CH, a.T, ga, ba, gb, bb, cf[0], cf[1], cf[2], cf[3]);
   } else if (ld.mode == LD_RESIDUAL) {
     gn_from_records(ld.gn, b, CH, a.T, cf[0], cf[1], dacc);
   }
-  __syncthreads();
+  lds_sync();
   const float afc = ld.af ? ld.af[(size_t)b * CH + c] : 1.f;
   float st[2] = {0.f, 0.f};
 #pragma unroll

@@ -12,7 +12,8 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsepvad.so")
+# SEPVAD_LIB: an alternative build of the same library (A/B timing of kernel variants, tools/ab.sh)
+LIB_PATH = os.environ.get("SEPVAD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsepvad.so")
 
 SEPVAD_LN_PLAIN, SEPVAD_LN_RECURSIVE, SEPVAD_LN_RESIDUAL = 0, 1, 2
 SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3 = 0, 1

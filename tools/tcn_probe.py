@@ -33,6 +33,10 @@ def main(path):
             x1, x2 = full[:, 1, 15], full[:, 2, 15]  # after the XCD exchange; after the input statistics
             print(f"  prologue: first-touch loads + XCD exchange {np.median(x1 - ent):.2f}, record sums "
                   f"{np.median(x2 - x1):.2f}, input LN {np.median(st[:, 0, 0] - x2):.2f} us (medians)")
+        if nblk > 7 and (full[:, 6, 15] > 0).all() and (full[:, 7, 15] > 0).all():
+            x6, x7 = full[:, 6, 15], full[:, 7, 15]  # loads issued; LN records (and every earlier load) landed
+            print(f"    entry -> loads issued {np.median(x6 - ent):.2f}, -> loads landed {np.median(x7 - x6):.2f} "
+                  f"(max {(x7 - x6).max():.2f}), -> XCD exchange done {np.median(full[:, 1, 15] - x7):.2f} us")
     if nblk > 5 and (full[:, 3:6, 15] > 0).all() and (ent > 0).all():
         c3, c4, c5 = (full[:, k, 15] * 100.0 for k in (3, 4, 5))  # s_memtime ticks (undo the /100)
         wp = st[:, 0, 0] - ent
