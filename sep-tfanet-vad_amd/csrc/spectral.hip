@@ -26,7 +26,18 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 __device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
 
 // One radix-4 Stockham stage (stride Ns) of a 256-point transform, one wave (lane = j).
-template <bool INV>
+// Twiddle W512^idx, idx in [0, 512). HALF: the table holds only W512^0..255 (W512^(x+256) = -W512^x).
+template <bool HALF>
+__device__ __forceinline__ float2 twid(const float2* tw, int idx) {
+  if constexpr (HALF) {
+    const float2 w = tw[idx & 255];
+    return idx < 256 ? w : make_float2(-w.x, -w.y);
+  } else {
+    return tw[idx];
+  }
+}
+
+template <bool INV, bool HALF = false>
 __device__ __forceinline__ void fft_stage(const float2* in, float2* out, const float2* tw, int lane, int Ns) {
   const int j = lane;
   const int k = j & (Ns - 1);
@@ -36,7 +47,7 @@ __device__ __forceinline__ void fft_stage(const float2* in, float2* out, const f
   if (Ns > 1) {
 #pragma unroll
     for (int r = 1; r < 4; ++r) {
-      float2 w = tw[2 * ((r * k * (64 / Ns)) & 255)];  // W_256^(r k 64/Ns) = W_512^(2 ...)
+      float2 w = twid<HALF>(tw, 2 * ((r * k * (64 / Ns)) & 255));  // W_256^(r k 64/Ns) = W_512^(2 ...)
       if (INV) w.y = -w.y;
       v[r] = cmul(v[r], w);
     }
@@ -61,15 +72,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // 256-point transform of one wave ping-ponging between its buffers b0 and b1 (4 stages: result back
 // in b0); the caller's buffers must be complete for this wave (wave_lds_sync or a barrier) on entry.
-template <bool INV>
+template <bool INV, bool HALF = false>
 __device__ inline void fft256(float2* b0, float2* b1, const float2* tw, int lane) {
-  fft_stage<INV>(b0, b1, tw, lane, 1);
+  fft_stage<INV, HALF>(b0, b1, tw, lane, 1);
   wave_lds_sync();
-  fft_stage<INV>(b1, b0, tw, lane, 4);
+  fft_stage<INV, HALF>(b1, b0, tw, lane, 4);
   wave_lds_sync();
-  fft_stage<INV>(b0, b1, tw, lane, 16);
+  fft_stage<INV, HALF>(b0, b1, tw, lane, 16);
   wave_lds_sync();
-  fft_stage<INV>(b1, b0, tw, lane, 64);
+  fft_stage<INV, HALF>(b1, b0, tw, lane, 64);
   wave_lds_sync();
 }
 
@@ -253,12 +264,15 @@ hipError_t launch_vad1(const Vad1Args& a, hipStream_t s) {
 // iSTFT: one workgroup (8 waves) per (utterance*speaker, chunk of IS_OWN frames). Computes frames
 // [f0-1, f0+IS_OWN) (one halo frame) and owns output hop-segments [f0, f0+IS_OWN) (+ segment T for
 // the last chunk). Segment j = padded samples [256 j, 256 j + 256); output n = p - 256.
+// LDS <= 53 KB (three workgroups per CU): half twiddle table, the window read through the cache, and the
+// mask side-output staging aliased onto the FFT work buffers (the two are live in different phases).
 __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
-  __shared__ float2 tw[512];
-  __shared__ float win[NFFT];
+  __shared__ float2 tw[256];
   __shared__ float2 spec[IS_FR][NBIN + 1];   // est of the computed frames; later their time samples
-  __shared__ float mk[IS_FR][NBIN];           // sigmoid(mask) (side output)
   __shared__ float2 work[8][M256];
+  static_assert(IS_OWN * NBIN * sizeof(float) <= sizeof(work), "mask staging fits the work buffers");
+  float (*mk)[NBIN] = reinterpret_cast<float (*)[NBIN]>(&work[0][0]);  // sigmoid(mask) of owned frame fo+1 at row fo
+  const float* win = a.window;
   __shared__ float yn[4][IS_FR + 6];          // GN'd VAD features, frames fbeg-3 .. fbeg+IS_FR+2
   __shared__ float vadv[IS_FR + 4];           // vad at frames fbeg-2 .. fbeg+IS_FR+1
   __shared__ float gain[IS_FR];
@@ -269,7 +283,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
   const int T = a.T;
   const int b = bs / a.S, s = bs % a.S;
   const int fbeg = f0 - 1;
-  for (int i = tid; i < 512; i += 512) { tw[i] = a.tw[i]; win[i] = a.window[i]; }
+  if (tid < 256) tw[tid] = a.tw[tid];
 
   // Every input load of the block is issued up front (forward mode): the X / mask rows of the computed
   // frames into registers, the VAD features, then the BN_1 records. The block then waits once instead
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
         const float m = ok ? sigmoid_f(mr[j]) : 0.f;
         const float g = gain[fi];
         spec[fi][k] = ok ? make_float2(g * (xr[j].x * m), g * (xr[j].y * m)) : make_float2(0.f, 0.f);
-        mk[fi][k] = m;
+        if (fi > 0) mk[fi - 1][k] = m;
       }
     }
   } else {
@@ -364,7 +378,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       float2 e = make_float2(0.f, 0.f);
       if (f >= 0 && f < T) e = a.est_in[((size_t)bs * NBIN + k) * T + f];
       spec[fi][k] = e;
-      mk[fi][k] = 0.f;
+      if (fi > 0) mk[fi - 1][k] = 0.f;
     }
   }
   lds_sync();
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
       const int i = min(tid + j * 512, NBIN * IS_OWN - 1);
       const int k = i / IS_OWN, fo = i - k * IS_OWN;
       ev[j] = spec[fo + 1][k];
-      mv[j] = mk[fo + 1][k];
+      mv[j] = mk[fo][k];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
     }
     wave_lds_sync();
     // ping-pong with the (now consumed) spec row of this frame; result lands in w0
-    fft256<true>(w0, Y, tw, lane);
+    fft256<true, true>(w0, Y, tw, lane);
     float* fr = reinterpret_cast<float*>(Y);  // time samples overwrite the frame's spectrum row
     const float sc = 1.f / 256.f;             // 1/N of the 512-point c2r == 1/256 on the half-length transform
 #pragma unroll
