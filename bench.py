@@ -202,12 +202,11 @@ def main():
     import sep_tfanet_vad_amd as pkg
     from sep_tfanet_vad_amd import synth
     cfg = pkg.CONFIG_WITH_VAD
-    net = pkg.SeparationModel(**cfg) if rank == 0 else None
-    if net is None:
-        import contextlib
-        import io
-        with contextlib.redirect_stdout(io.StringIO()):
-            net = pkg.SeparationModel(**cfg)
+    import contextlib
+    # the constructor prints the merged config like the reference (model/model.py:371); keep stdout
+    # to the single JSON line the driver parses
+    with contextlib.redirect_stdout(sys.stderr):
+        net = pkg.SeparationModel(**cfg)
     sd = synth.make_state_dict(cfg, 1234)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     net = net.eval().to(dev)
