@@ -1,18 +1,22 @@
 """Throughput of the MI355X Sep-TFAnet^VAD forward path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f16x3|fp32|bf16|f16] [--workload offline|stream]
 
 One step = one ``SeparationModel.forward`` (config_with_vad.json) over a resident batch of 64
 synthetic 2-speaker mixtures of 32 000 samples (4 s @ 8 kHz resampled to 16 kHz by the
-reference's CLI, only_inference.py:76-79 => T = 126 frames) per GPU. For N > 1 the driver launches
-one process per GPU (torchrun); every rank runs its own shard of utterances (weak scaling, no
-collective on the data path, only barriers around the timed region). Rank 0 prints one JSON line.
+reference's CLI, only_inference.py:76-79 => T = 126 frames) per GPU. One process per GPU: the
+driver launches the ranks with torch.distributed.run; ``--gpus N`` without a torchrun environment
+starts them itself (a child torch.distributed.run, before this process touches the GPU). Every rank
+runs its own shard of utterances (weak scaling, no collective on the data path, only barriers around
+the timed region and a max-reduce of the elapsed time). Rank 0 prints one JSON line.
 
 Extra fields:
-  roofline      dominant kernel = DepthConv1d.res_out GEMM (512->256, fp32 MFMA); algorithmic FLOPs
-                per launch / its average launch time, from HIP events recorded by libsepvad on the
-                stream the kernels run on, during the timed steps.
-  cpu_baseline  the oracle CPU restatement (oracle/torch_ref.py, torch fp32) on the host cores,
+  roofline      dominant kernel = k_tcn, the fused persistent TCN (24 blocks of conv1d 256->256, depthwise
+                conv, res_out 512->256, TF-attention, recursive LN in one launch); algorithmic FLOPs per
+                launch (its two pointwise GEMMs per block) / its average launch time from HIP events that
+                libsepvad records on the stream the kernel runs on. On the multi-kernel
+                schedule (fp32 GEMMs, T > 256) the res_out GEMM.
+  cpu_baseline  the oracle CPU restatement (oracle/torch_ref.py, torch fp32) on all host cores,
                 rank 0 at N=1 only, on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -20,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -77,7 +83,7 @@ def cpu_baseline(seconds: float = 12.0):
     from oracle.torch_ref import OracleModel
     import sep_tfanet_vad_amd as pkg
     from sep_tfanet_vad_amd import synth
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    threads = os.cpu_count() or 1  # every host core, stated in the line
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234).items()}
     om = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float32)
@@ -96,20 +102,75 @@ def cpu_baseline(seconds: float = 12.0):
                        f"in {el:.1f} s, oracle/torch_ref.py fp32 on {threads} threads")
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) outside a torchrun environment: run N ranks, one process per GPU, as a child
+    ``torch.distributed.run`` and return its exit code. Called before anything touches the GPU (this
+    process never initialises HIP, so nothing is exec'd from a GPU process). None = run in-process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def init_dist(args, backend="nccl"):
+    """(dist or None, world, rank, local_rank) of this rank; world must equal --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    d = None
+    if world > 1:
+        import torch.distributed as d
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            d.init_process_group(backend, device_id=torch.device("cuda", local_rank))
+        else:
+            d.init_process_group(backend)
+    return d, world, rank, local_rank
+
+
+def timed_region(step, steps, warmup, dist=None, sync=lambda: None, reduce_device="cpu"):
+    """W untimed warmup steps, then EXACTLY `steps` steps bracketed by a barrier + device sync on both
+    sides; returns the elapsed seconds, max over ranks (the driver contract)."""
+    for _ in range(warmup):
+        step()
+    sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        sync()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=reduce_device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
 def bench_stream(args):
     """BASELINE cfg 3: OnlineSaving (model/online_class_unknown_targets.py:72-105) over 256 streams of
     4 s @ 16 kHz, 3 s windows at a 160 ms hop (7 windows per stream, each a batched B=256 forward of
     48 000 samples, T=188), PIT-L1 realignment and stitching on the device. One step = one calc_online
     over all streams. value = stream-windows/s (whole job); audio_seconds_per_second = value * save_sec
     (seconds of new audio emitted per wall-clock second, all streams together)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dist, world, rank, local_rank = init_dist(args)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     import contextlib
@@ -133,23 +194,7 @@ def bench_stream(args):
     def step():
         ons.calc_online(x, "bench", 10 ** 6, ikw)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev)
     if rank == 0:
         windows = world * n_streams * n_win * args.steps
         out = {
@@ -185,17 +230,13 @@ def main():
     ap.add_argument("--workload", default="offline", choices=["offline", "stream"],
                     help="offline: cfg 2 (default, the BASELINE metric); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.workload == "stream":
         return bench_stream(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dist, world, rank, local_rank = init_dist(args)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
@@ -224,26 +265,8 @@ def main():
         with torch.no_grad():
             return net(x)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     # timed region (value)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev)
 
     # per-kernel timing pass (HIP events on the kernels' stream), same steps
     h.set_timing(True)

@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <unordered_map>
@@ -53,6 +55,8 @@ struct BlockOff {
   float a1, a2;
   int dil;
   double wsum[5];  // {Σγa, Σβa, Σβa², Σγa·βa, Σγa²} of ln_first (closed-form recursive-LN stats)
+  float sx;        // 2^-ex: fp16 range scale of the conv1d A operand (x'), undone by w1.scale (range guard)
+  float eps2;      // reg2 eps * 2^-2ed: d is produced scaled by 2^-ed (dconv weights/bias pre-scaled)
 };
 
 struct Workspace {
@@ -88,6 +92,20 @@ Workspace ws_view(const Workspace& w, int b0, int Tp) {
 
 constexpr int MAX_SPLIT = 4;
 
+// Per caller-stream state (include/sepvad.h: concurrent forwards on different streams of one handle are
+// allowed): the workspace, the fused TCN's hand-off words, launch salt and give-up words. Weights are
+// shared and read-only.
+struct StreamCtx {
+  void* stream = nullptr;
+  Workspace ws;
+  unsigned long long* tgran = nullptr;  // hand-off words [tcn_cap][2][NGR]
+  unsigned* terr = nullptr;             // device word: tag0 of the last launch whose hand-off wait gave up
+  unsigned* herr = nullptr;             // host-mapped copy (pinned, written by the kernel)
+  unsigned* herr_dev = nullptr;         // its device address
+  unsigned reported = 0;                // last give-up word already returned to the caller
+  unsigned tsalt = 0;                   // launch counter (hand-off tag salt)
+};
+
 }  // namespace
 
 struct sepvad_model {
@@ -107,7 +125,6 @@ struct sepvad_model {
   float v_a = 0.f, v_b2 = 0.f;
   size_t gate = 0;
   bool same_stft_window = true;
-  Workspace ws;
   // batch split: utterance chunks of one forward run concurrently on internal streams (fork/join
   // on the caller's stream); the chunks' kernels fill each other's ramp/drain bubbles
   int split = 1;
@@ -118,10 +135,13 @@ struct sepvad_model {
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU)
   __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered weights
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
-  unsigned long long* tgran = nullptr;  // hand-off words [tcn_cap][2][NGR]
-  unsigned* terr = nullptr;     // give-up flag of the last launches
-  unsigned tsalt = 0;           // launch counter (hand-off tag salt)
   bool last_fused = false;
+  float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
+  // caller-stream contexts (workspace, hand-off words, give-up words); `mu` serialises the host-side
+  // enqueue of concurrent callers (the kernels of different streams still overlap on the device)
+  std::vector<std::unique_ptr<StreamCtx>> ctx;
+  std::mutex mu;
+  int res_B = 0, res_N = 0;     // sepvad_reserve hint: every context's workspace is sized at least this
   unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
   // timing
   bool timing = false;
@@ -186,8 +206,9 @@ std::vector<float> fold_wn(const float* g, const float* v, int cout, int rest) {
 }
 
 // [cout][cin] fp32 -> zero-padded [mpad][cin] fp32 + the fp16 hi/lo split of each row scaled by
-// 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^e undoes it exactly.
-PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int cin, int mpad) {
+// 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^(e + col_e) undoes it exactly, and
+// also the 2^-col_e the GEMM applies to its A operand before splitting it (range guard, see range_exp).
+PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int cin, int mpad, int col_e = 0) {
   PackedW p;
   std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
   std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin);
@@ -198,7 +219,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
     int e = 0;
     if (mx > 0.f) { (void)std::frexp(mx, &e); }  // mx = f * 2^e, f in [0.5, 1)
     const float s = std::ldexp(1.f, -e);
-    sc[o] = std::ldexp(1.f, e);
+    sc[o] = std::ldexp(1.f, e + col_e);
     for (int i = 0; i < cin; ++i) {
       const float v = o < cout ? w[(size_t)o * cin + i] : 0.f;
       w32[(size_t)o * cin + i] = v;
@@ -232,12 +253,35 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   return p;
 }
 
-int ws_reserve(sepvad_model* h, int B, int N) {
+// Range guard of the fp16 split: an fp16 plane holds |x| up to 65504, and the lo plane
+// keeps full relative precision only for |x| >= 2^-3 (below that it becomes subnormal). Every A operand
+// of the pointwise GEMMs is an affine image of GroupNorm-normalised data (x' = GN_b(..) or o + GN_c(..),
+// d = PReLU(dconv(GN1(h))), the head's GN_out(PReLU(x'))), so its magnitude is fixed by the GN affines and
+// weights, not by the utterance: |y_k| <~ |gamma_k| * NSIG + |beta_k| for normalised values within NSIG.
+// Each operand is therefore scaled by a static power of two 2^-e that brings that bound into [0.5, 1)
+// and the inverse is folded into the weights' per-row scale (or, for d, into the dconv weights, with the
+// reg2 eps rescaled by 2^-2e): exact in fp32 arithmetic, bitwise neutral wherever nothing under- or
+// overflowed, and it keeps weights scaled by 1e-3 or 1e3 at fp32-equivalent accuracy (tests).
+constexpr double NSIG = 4.0;
+double gn_bound(const float* g, const float* b, int n) {
+  double m = 0.0;
+  for (int k = 0; k < n; ++k) m = std::max(m, std::fabs((double)g[k]) * NSIG + std::fabs((double)b[k]));
+  return m;
+}
+int range_exp(double bound) {
+  if (!(bound > 0.0) || !std::isfinite(bound)) return 0;
+  int e = 0;
+  (void)std::frexp(bound, &e);  // bound = f * 2^e, f in [0.5, 1)
+  return std::max(-60, std::min(60, e));
+}
+
+int ws_reserve(StreamCtx* c, int B, int N) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
-  if (B <= h->ws.Bmax && Tp <= h->ws.Tpmax) return SEPVAD_OK;
-  const int Bm = std::max(B, h->ws.Bmax), Tm = std::max(Tp, h->ws.Tpmax);
-  if (h->ws.base) { (void)hipFree(h->ws.base); h->ws.base = nullptr; }
+  Workspace& w = c->ws;
+  if (B <= w.Bmax && Tp <= w.Tpmax) return SEPVAD_OK;
+  const int Bm = std::max(B, w.Bmax), Tm = std::max(Tp, w.Tpmax);
+  if (w.base) { (void)hipFree(w.base); w.base = nullptr; w.Bmax = w.Tpmax = 0; }
   const size_t bt = (size_t)Bm * Tm;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
@@ -252,7 +296,6 @@ int ws_reserve(sepvad_model* h, int B, int N) {
   char* base = nullptr;
   HIPCHK(hipMalloc(&base, off));
   HIPCHK(hipMemset(base, 0, off));
-  Workspace& w = h->ws;
   w.base = base; w.bytes = off; w.Bmax = Bm; w.Tpmax = Tm;
   w.X = (float2*)(base + oX); w.specdb = (float*)(base + oSpec); w.S0 = (float*)(base + oS0);
   w.O[0] = (float*)(base + oO0); w.O[1] = (float*)(base + oO1); w.A = (float*)(base + oA);
@@ -289,6 +332,7 @@ int ev_record(sepvad_model* h, hipStream_t s) {
 
 void set_weights(const sepvad_model* h, GemmArgs& g, const PackedW& w) {
   g.prec = h->prec;
+  g.ascale = 1.f;
   g.W32 = h->P(w.w32);
   g.Whi = h->H(w.whi);
   g.Wlo = h->H(w.wlo);
@@ -350,6 +394,9 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     if (rec) { put(PB_LNBG, bo.lnb_g, CH); put(PB_LNBB, bo.lnb_b, CH); }
     put(PB_ATT, bo.attp, 20);
     q[PB_A1] = bo.a1; q[PB_A2] = bo.a2;
+    q[PB_SX] = bo.sx;
+    q[PB_SXN] = i + 1 < h->nblk ? h->blk[i + 1].sx : 1.f;
+    q[PB_EPS2] = bo.eps2;
     std::memcpy(q + PB_WSUM, bo.wsum, sizeof(bo.wsum));
     const int li = i % h->cfg.layer;
     if (bo.dil != (li == 0 ? 1 : (li % 4 + 1))) { g_err = "fused TCN: dilation schedule mismatch"; return SEPVAD_E_ARG; }
@@ -358,10 +405,51 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->tprm, pb.size() * sizeof(float)));
   HIPCHK(hipMemcpy(h->tprm, pb.data(), pb.size() * sizeof(float), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&h->tgran, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(h->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long)));
-  HIPCHK(hipMalloc(&h->terr, 16));
-  HIPCHK(hipMemset(h->terr, 0, 16));
+  return SEPVAD_OK;
+}
+
+void free_ctx(StreamCtx* c) {
+  if (c->ws.base) (void)hipFree(c->ws.base);
+  if (c->tgran) (void)hipFree(c->tgran);
+  if (c->terr) (void)hipFree(c->terr);
+  if (c->herr) (void)hipHostFree(c->herr);
+  delete c;
+}
+
+// The context of caller stream `stream` (created on first use; the caller holds h->mu).
+int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
+  for (auto& c : h->ctx)
+    if (c->stream == stream) { *out = c.get(); return SEPVAD_OK; }
+  std::unique_ptr<StreamCtx, void (*)(StreamCtx*)> c(new StreamCtx(), free_ctx);
+  c->stream = stream;
+  if (h->tcn_cap > 0) {
+    const size_t gb = (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long);
+    HIPCHK(hipMalloc(&c->tgran, gb));
+    HIPCHK(hipMemset(c->tgran, 0, gb));
+  }
+  HIPCHK(hipMalloc(&c->terr, 16));
+  HIPCHK(hipMemset(c->terr, 0, 16));
+  HIPCHK(hipHostMalloc((void**)&c->herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(c->herr, 0, 64);
+  HIPCHK(hipHostGetDevicePointer((void**)&c->herr_dev, c->herr, 0));
+  if (h->res_B > 0) {
+    const int rc = ws_reserve(c.get(), h->res_B, h->res_N);
+    if (rc) return rc;
+  }
+  *out = c.get();
+  h->ctx.emplace_back(c.release());
+  return SEPVAD_OK;
+}
+
+// Give-up words written by k_tcn launches of this context that completed since the last check: report
+// each once (the word holds the failing launch's salt, so a later give-up is a new value).
+int check_giveup(StreamCtx* c) {
+  const unsigned v = __atomic_load_n(c->herr, __ATOMIC_ACQUIRE);
+  if (v != 0 && v != c->reported) {
+    c->reported = v;
+    return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up in an earlier forward on this stream "
+                              "(that forward's outputs are invalid)");
+  }
   return SEPVAD_OK;
 }
 
@@ -417,12 +505,14 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     }
     h->tw = pk.add(tw);
   }
+  double xbound = 0.0;  // range bound of the current block's x' (range guard)
   {
     const float* lg = get("TCN.LN.weight", CH);
     const float* lb = get("TCN.LN.bias", CH);
     BAIL();
     h->ln_g = pk.add(lg, CH);
     h->ln_b = pk.add(lb, CH);
+    xbound = gn_bound(lg, lb, CH);  // x'_0 = TCN.LN(S0)
   }
   // blocks (model/model.py:285-295,103-127,182-195,310-319)
   for (int i = 0; i < h->nblk; ++i) {
@@ -444,12 +534,31 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const float* r2g = get(p + ".reg2.weight", HID);
     const float* r2b = get(p + ".reg2.bias", HID);
     BAIL();
-    bo.w1 = pack_pointwise(pk, fold_wn(g1, v1, CH, CH), CH, CH, CH);
+    const int ex = range_exp(xbound);
+    bo.sx = std::ldexp(1.f, -ex);
+    bo.w1 = pack_pointwise(pk, fold_wn(g1, v1, CH, CH), CH, CH, CH, ex);
     bo.b1 = pk.add(b1, CH);
     bo.g1 = pk.add(r1g, CH);
     bo.be1 = pk.add(r1b, CH);
-    bo.wd = pk.add(fold_wn(gd, vd, HID, 3));
-    bo.bd = pk.add(bd, HID);
+    {
+      // d = PReLU(dconv(GN1(h))) produced pre-scaled by 2^-ed: dconv weights and bias scaled (exact), the
+      // reg2 GroupNorm eps scaled by 2^-2ed so GN2(d) is unchanged (range guard)
+      std::vector<float> wd = fold_wn(gd, vd, HID, 3), bds(bd, bd + HID);
+      double dbound = 0.0;
+      for (int j = 0; j < HID; ++j) {
+        const int k = j / 2;  // groups = CH, depth multiplier 2 (model/model.py:110-113)
+        const double nb = std::fabs((double)r1g[k]) * NSIG + std::fabs((double)r1b[k]);
+        const double sw = std::fabs((double)wd[3 * j]) + std::fabs((double)wd[3 * j + 1]) + std::fabs((double)wd[3 * j + 2]);
+        dbound = std::max(dbound, sw * nb + std::fabs((double)bd[j]));
+      }
+      dbound *= std::max(1.0, std::fabs((double)a2[0]));
+      const int ed = range_exp(dbound);
+      for (auto& v : wd) v = std::ldexp(v, -ed);
+      for (auto& v : bds) v = std::ldexp(v, -ed);
+      bo.wd = pk.add(wd);
+      bo.bd = pk.add(bds);
+      bo.eps2 = std::ldexp(1e-8f, -2 * ed);
+    }
     {
       // reg2 (GroupNorm(1, H) of d, model/model.py:136) folded out of the res_out operand: see gemm.hip
       const std::vector<float> w2 = fold_wn(g2, v2, CH, HID);
@@ -499,6 +608,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       BAIL();
       bo.lna_g = pk.add(fa, CH); bo.lna_b = pk.add(fb, CH);
       bo.lnb_g = pk.add(sa, CH); bo.lnb_b = pk.add(sb, CH);
+      xbound = gn_bound(sa, sb, CH);  // next block's x' = GN_b(..)
       for (int j = 0; j < 5; ++j) bo.wsum[j] = 0.0;
       for (int k = 0; k < CH; ++k) {
         const double g = fa[k], e = fb[k];
@@ -509,6 +619,9 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       const float* fb = get("TCN.ln_modules." + std::to_string(i) + ".bias", CH);
       BAIL();
       bo.lna_g = pk.add(fa, CH); bo.lna_b = pk.add(fb, CH);
+      xbound += gn_bound(fa, fb, CH);  // next block's x' = o + GN_c(..)
+    } else {
+      xbound = 0.0;  // plain residual add: no static bound, no scale
     }
     h->blk.push_back(bo);
   }
@@ -524,7 +637,9 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     h->out_a = oa[0];
     h->out_g = pk.add(og, CH);
     h->out_b = pk.add(ob, CH);
-    h->wout = pack_pointwise(pk, fold_wn(gg, vv, MOUT, CH), MOUT, CH, MOUT_PAD);
+    const int eh = range_exp(gn_bound(og, ob, CH));  // head A operand = GN_out(PReLU(x'))
+    h->out_sx = std::ldexp(1.f, -eh);
+    h->wout = pack_pointwise(pk, fold_wn(gg, vv, MOUT, CH), MOUT, CH, MOUT_PAD, eh);
     std::vector<float> bpad(MOUT_PAD, 0.f);
     std::memcpy(bpad.data(), bb, MOUT * sizeof(float));
     h->bo = pk.add(bpad);
@@ -594,7 +709,13 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
 int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N) {
   if (!h || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_reserve: bad arguments");
   DeviceGuard dg(h->device);
-  return ws_reserve(h, B, N);
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->res_B = std::max(h->res_B, (int)B);
+  h->res_N = std::max(h->res_N, (int)N);
+  StreamCtx* c0 = nullptr;
+  int rc = get_ctx(h, nullptr, &c0);  // the default stream's context exists from here on
+  for (size_t i = 0; rc == SEPVAD_OK && i < h->ctx.size(); ++i) rc = ws_reserve(h->ctx[i].get(), h->res_B, h->res_N);
+  return rc;
 }
 
 int32_t sepvad_set_precision(sepvad_handle h, int32_t precision) {
@@ -627,7 +748,12 @@ namespace {
 // the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G && h->tgran != nullptr;
+  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
 }
 
 // Per-forward timing state (sepvad_set_timing): HIP events around the GEMM launches of chunk 0.
@@ -636,12 +762,12 @@ struct TimingRec {
 };
 
 // Enqueues the forward of utterances [b0, b0 + B) on stream s (model/model.py:402-461).
-int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N, const SepVadOutputs* out,
-                  const SepVadInferKw* kw, hipStream_t s, TimingRec* tr) {
+int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b0, int B, int N,
+                  const SepVadOutputs* out, const SepVadInferKw* kw, hipStream_t s, TimingRec* tr) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
   const SepVadConfig& c = h->cfg;
-  const Workspace w = ws_view(h->ws, b0, Tp);
+  const Workspace w = ws_view(cx->ws, b0, Tp);
   const int ntu = Tp / TILE;
   x += (size_t)b0 * ldx;
   const size_t u2 = (size_t)b0 * 2;
@@ -685,12 +811,16 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
     ta.tf_att = c.tf_attention;
     ta.wfrag = h->twf; ta.prm = h->tprm;
     ta.alpha_h = h->out_a;
-    ta.gran = h->tgran; ta.err = h->terr;
-    ta.xmode = getenv("SEPVAD_TCN_XMODE") ? atoi(getenv("SEPVAD_TCN_XMODE")) : 0;
+    ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
+    ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
+    ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
+    ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     int ngroups = std::min(B, h->tcn_cap / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + 4 per block per utterance, < 2^TCN_EPOCH_BITS
-    const int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / (4 * h->nblk);
+    // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)
+    int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / (4 * h->nblk);
+    if (const int mi = env_int("SEPVAD_TCN_MAX_ITER", 0)) max_iter = std::min(max_iter, mi);
     if (max_iter < 1) return fail(SEPVAD_E_ARG, "fused TCN: too many blocks");
     const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
@@ -700,12 +830,12 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
       const int ng = std::min(ngroups, Bl);
       const int ngl = ng >= 8 ? ng - ng % 8 : ng;
       // tag salt: never 0; hand-off words re-zeroed when the 20-bit salt wraps
-      h->tsalt = (h->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
-      if (h->tsalt == 0) {
-        HIPCHK(hipMemsetAsync(h->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
-        h->tsalt = 1;
+      cx->tsalt = (cx->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
+      if (cx->tsalt == 0) {
+        HIPCHK(hipMemsetAsync(cx->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
+        cx->tsalt = 1;
       }
-      ta.tag0 = h->tsalt << TCN_EPOCH_BITS;
+      ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
       ta.B = Bl;
       ta.S0 = w.S0 + (size_t)u0 * Tp * CH;
       ta.ln = gn_src(w.rec_gate + (size_t)u0 * (Tp / GATE_ROWS) * 2, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
@@ -739,6 +869,7 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
     GemmArgs g{};
     g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
     set_weights(h, g, h->wout);
+    g.ascale = h->out_sx;
     g.bias = h->P(h->bo);
     g.ld.mode = LD_PLAIN; g.ld.X = w.O[0];
     g.ld.head = 1; g.ld.alpha_h = h->out_a;
@@ -757,6 +888,7 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
       GemmArgs g{};
       g.B = B; g.T = T; g.Tp = Tp; g.M = CH; g.Mreal = CH; g.K = CH; g.ldy = CH;
       set_weights(h, g, bo.w1);
+      g.ascale = bo.sx;
       g.bias = h->P(bo.b1); g.prelu = bo.a1;
       if (i == 0) {
         g.ld.mode = LD_GN; g.ld.X = w.S0;   // TCN.LN (model/model.py:333)
@@ -791,7 +923,7 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
       } else {
         g2.ld.mode = LD_PLAIN; g2.ld.X = w.D32;
       }
-      g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, 1e-8f);
+      g2.fold = gn_src(w.rec_dw, Tp / STAT_ROWS, 2, 0, nullptr, nullptr, bo.eps2);  // d pre-scaled (range guard)
       g2.foldK = HID; g2.foldc = h->P(bo.fc2);
       g2.Y = w.R; g2.colsum = w.colsum; g2.rowsum = w.rowsum;
       if (probing && i == h->probe_blk) g2.probe = h->probe + g1_grid * PROBE_SLOTS;
@@ -822,6 +954,7 @@ int enqueue_chunk(sepvad_model* h, const float* x, int ldx, int b0, int B, int N
       GemmArgs g{};
       g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
       set_weights(h, g, h->wout);
+      g.ascale = h->out_sx;
       g.bias = h->P(h->bo);
       g.ld = residual_spec(h, w, h->nblk - 1, w.O[cur], w.R, Tp);
       g.ld.head = 1; g.ld.alpha_h = h->out_a;
@@ -872,7 +1005,12 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
                  const SepVadInferKw* kw, hipStream_t s) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
-  int rc = ws_reserve(h, B, N);
+  StreamCtx* cx = nullptr;
+  int rc = get_ctx(h, (void*)s, &cx);
+  if (rc) return rc;
+  rc = check_giveup(cx);  // an earlier forward on this stream whose k_tcn gave up: report it now
+  if (rc) return rc;
+  rc = ws_reserve(cx, B, N);
   if (rc) return rc;
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   h->ev.clear();
@@ -894,7 +1032,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   TimingRec tr;
   if (nsplit == 1) {
     if (ev_record(h, s)) return SEPVAD_E_HIP;
-    rc = enqueue_chunk(h, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr);
+    rc = enqueue_chunk(h, cx, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr);
     if (rc) return rc;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
   } else {
@@ -904,7 +1042,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
     for (int k = 0; k < nsplit; ++k) {
       const int bc = B / nsplit + (k < B % nsplit ? 1 : 0);
       HIPCHK(hipStreamWaitEvent(h->sub[k], h->fork, 0));
-      rc = enqueue_chunk(h, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr);
+      rc = enqueue_chunk(h, cx, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr);
       if (rc) return rc;
       HIPCHK(hipEventRecord(h->join[k], h->sub[k]));
       HIPCHK(hipStreamWaitEvent(s, h->join[k], 0));
@@ -955,6 +1093,7 @@ int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int
   if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
   if (ldx < N || ldx > INT32_MAX) return fail(SEPVAD_E_SHAPE, "sepvad_forward: row stride must be >= N");
   DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
   return forward_impl(h, x, (int)ldx, B, N, out, kw, (hipStream_t)stream);
 }
 
@@ -972,16 +1111,15 @@ int32_t sepvad_set_fused(sepvad_handle h, int32_t on) {
 int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
   DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
   if (used) *used = h->last_fused ? 1 : 0;
-  if (!h->terr) return SEPVAD_OK;
   HIPCHK(hipDeviceSynchronize());
-  unsigned err = 0;
-  HIPCHK(hipMemcpy(&err, h->terr, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) {
-    HIPCHK(hipMemset(h->terr, 0, 16));
-    return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up (outputs invalid)");
+  int rc = SEPVAD_OK;
+  for (auto& c : h->ctx) {
+    const int r = check_giveup(c.get());
+    if (r && rc == SEPVAD_OK) rc = r;
   }
-  return SEPVAD_OK;
+  return rc;
 }
 
 int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {
@@ -1104,12 +1242,10 @@ void sepvad_destroy(sepvad_handle h) {
     if (h->join[k]) (void)hipEventDestroy(h->join[k]);
   }
   if (h->fork) (void)hipEventDestroy(h->fork);
-  if (h->ws.base) (void)hipFree(h->ws.base);
+  for (auto& c : h->ctx) free_ctx(c.release());
   if (h->twf) (void)hipFree(h->twf);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
-  if (h->tgran) (void)hipFree(h->tgran);
-  if (h->terr) (void)hipFree(h->terr);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);
   delete h;

@@ -106,10 +106,17 @@ __device__ __forceinline__ double dword2(unsigned lo, unsigned hi) {
   return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
 }
 // Poll the N words p[k] (nullptr = none) until every tag equals `tag`; values into v[k]. All loads of a
-// pass are in flight together. Bounded: gives up (sets *err) after ~2^20 passes or once *err is set, and
-// the launch then runs to completion with invalid outputs instead of hanging.
+// pass are in flight together. Bounded: gives up after a.spin_limit passes, or as soon as another
+// workgroup of this launch gave up (the device word then holds this launch's tag0), and records the give-up
+// in the device word and in its host-mapped copy; the launch then runs to completion with invalid outputs
+// instead of hanging, and the host reports it (sepvad_forward / sepvad_fused_status). Words of earlier
+// launches' give-ups hold other tags, so a give-up never leaks into a later launch.
+__device__ __forceinline__ void giveup(const TcnArgs& a) {
+  __hip_atomic_store(a.err, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.herr != nullptr) __hip_atomic_store(a.herr, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 template <int N>
-__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], unsigned* err) {
+__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], const TcnArgs& a) {
   unsigned spins = 0;
   for (;;) {
     bool ok = true;
@@ -124,8 +131,8 @@ __device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, un
     if (ok) return;
     __builtin_amdgcn_s_sleep(1);
     if ((++spins & 255u) == 0 &&
-        (spins > (1u << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
+      giveup(a);
       return;
     }
   }
@@ -335,6 +342,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     a.probe[(size_t)blockIdx.x * a.nblk * 16 + 15] = wall_clock64();
     if (a.nblk > 5) a.probe[((size_t)blockIdx.x * a.nblk + 3) * 16 + 15] = __builtin_amdgcn_s_memtime();
   }
+  if (a.force_err && blockIdx.x == 0 && threadIdx.x == 0) giveup(a);  // diagnostics: report path only
   if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact
     if (tid < CH) sm.af[tid] = 1.f;
     if (tid < FR) sm.at[tid] = 1.f;
@@ -361,7 +369,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     {
     const int m = mu_, tid = tidu;
     auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4u; };
-    float raw[16], pg[2], pb[2];
+    float raw[16], pg[2], pb[2], sx0;
     {
       // buffer loads off one lane offset, the row as a constant offset (flat loads here got a fresh address
       // pair per row and were serialized by s_waitcnt vmcnt(0) on register reuse, ~1.5 us each). All
@@ -381,6 +389,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pg[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, co, 0, 0));
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
+      sx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc_of(ka->prm), 0, PB_SX * 4, 0));
       prefetch_w(w1h, w1l, voffu, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -394,7 +403,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       if (tid == 0) gput(slot(g, 1), a.tag0 + 1, xcc, false);
       const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
       unsigned v[1];
-      gpoll<1>(p, a.tag0 + 1, v, a.err);
+      gpoll<1>(p, a.tag0 + 1, v, a);
       if (tid < G) sm.gw[tid] = v[0];
       __syncthreads();
       bool same = a.xmode == 0;
@@ -420,7 +429,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int tl = trow(r);
         o[r] = fmaf(raw[r], s, h) * (t0 + tl < T ? 1.f : 0.f);
-        split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
+        split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
       }
     }
     __syncthreads();
@@ -509,7 +518,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         const int sk = tid - (NTHR - 4 * G);  // last 4G threads: GN1 words of member sk/4
         p[4] = sk >= 0 ? slot(sk >> 2, e1) + GW_STAT + (sk & 3) : nullptr;
-        gpoll<5>(p, tag1, v, a.err);
+        gpoll<5>(p, tag1, v, a);
       TPROBE(3);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       {
         const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
         unsigned v[1];
-        gpoll<1>(p, tag2, v, a.err);
+        gpoll<1>(p, tag2, v, a);
         if (tid < 4 * G) sm.gw[tid] = v[0];
         __syncthreads();  // also: every wave is done reading d from LDS
       TPROBE(6);
@@ -607,7 +616,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float fmu, frs;
         {
           const double2 acc = member_sums2(sm.gw, G, lane);  // every member's GN2 sums, member order
-          gn_moments(acc.x, acc.y, (double)HID * T, 1e-8f, fmu, frs);
+          gn_moments(acc.x, acc.y, (double)HID * T, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
         }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
         float rsum = 0.f, csr[16];
@@ -653,7 +662,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             const int tl = mi - 4, t = t0 + tl;
             if (t >= 0 && t < T) pp[0] = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
           }
-          gpoll<FG_MAX>(pp, tag3, v, a.err);
+          gpoll<FG_MAX>(pp, tag3, v, a);
           __syncthreads();  // csum complete (read below by other threads)
           if (tid < CH) {
             float s = 0.f;
@@ -728,7 +737,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int k = tid;  // word k % 22 of member k / 22
           const u64* pp[1] = {k < 2 * NMOM * G ? slot(k / (2 * NMOM), e4) + GW_STAT + k % (2 * NMOM) : nullptr};
           unsigned v[1];
-          gpoll<1>(pp, tag4, v, a.err);
+          gpoll<1>(pp, tag4, v, a);
           if (k < 2 * NMOM * G) sm.gw[k] = v[0];
         }
       TPROBE(11);
@@ -765,13 +774,16 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         prefetch_w(rsrc_of(wn), rsrc_of(wn + WF_W1L), voff1, rh, rl);
       }
       TPROBE(14);
-      // x' = next block input: o (registers) and the conv1d A operand (LDS)
+      // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
+      {
+        const float sxn = pm[PB_SXN];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int tl = trow(r);
-        const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
-        o[r] = (t0 + tl < T) ? x : 0.f;
-        split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r]);
+        for (int r = 0; r < 16; ++r) {
+          const int tl = trow(r);
+          const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
+          o[r] = (t0 + tl < T) ? x : 0.f;
+          split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sxn);
+        }
       }
       __syncthreads();
       TPROBE(12);

@@ -135,7 +135,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   auto put_a = [&](int row, int col, const float4& v) {  // 4 consecutive k at (row, col)
     if constexpr (PREC == PREC_F16X3) {
       uint2 hi, lo;
-      split4(v, hi, lo);
+      const float s = a.ascale;  // power-of-two range guard, undone exactly by wscale (api.hip)
+      split4(make_float4(v.x * s, v.y * s, v.z * s, v.w * s), hi, lo);
       *reinterpret_cast<uint2*>(&sm.Ahi[row][col]) = hi;
       *reinterpret_cast<uint2*>(&sm.Alo[row][col]) = lo;
     } else {

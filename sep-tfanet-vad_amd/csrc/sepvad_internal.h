@@ -79,6 +79,8 @@ struct GemmArgs {
   const float* wscale;                     // [M] 2^e_m (F16X3)
   const float* bias;                       // [M]
   float prelu;
+  float ascale;         // F16X3: power-of-two scale of the A operand before the fp16 split (range guard;
+                        // undone exactly by wscale, which carries the inverse)
   LoadSpec ld;
   float* Xmat;          // nullable: transformed A operand x' written once (by m-tile 0), [B][Tp][K]
   float* Y;             // [B][Tp][ldy]
@@ -236,7 +238,9 @@ constexpr int PB_WS2 = 3072, PB_B2 = 3328, PB_FC2 = 3584;          // res_out ro
 constexpr int PB_LNAG = 3840, PB_LNAB = 4096, PB_LNBG = 4352, PB_LNBB = 4608;  // ln_first / ln_second (or ln_modules)
 constexpr int PB_ATT = 4864;                                       // TF_Attention taps [20] (see AttStatsArgs)
 constexpr int PB_A1 = 4884, PB_A2 = 4885;                          // PReLU slopes
+constexpr int PB_SX = 4886, PB_SXN = 4887;                         // fp16 range scale of this / the next block's x'
 constexpr int PB_WSUM = 4888;                                      // 5 doubles (8-byte aligned)
+constexpr int PB_EPS2 = 4898;                                      // reg2 eps, rescaled with d (see api.hip range guard)
 constexpr int PB_SIZE = 4900;                                      // multiple of 4 (float4 staging)
 // fp16 hi/lo weights of one block in MFMA fragment order: conv1d hi | lo (256x256) | res_out hi | lo (256x512)
 constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
@@ -251,7 +255,10 @@ struct TcnArgs {
   double* rec_head;      // [B][G][2] (sum, sumsq) of PReLU(x') per member
   unsigned long long* gran;  // hand-off words [grid][2][NGR]
   unsigned tag0;         // launch salt << TCN_EPOCH_BITS (tags of this launch: tag0 + epoch, epoch >= 1)
-  unsigned* err;         // give-up flag (sticky until sepvad_fused_status reads it)
+  unsigned* err;         // device word: tag0 of the last launch on this stream context whose hand-off wait gave up
+  unsigned* herr;        // host-mapped (pinned) copy of the same word, read by the host without a sync
+  unsigned spin_limit;   // poll passes before a wait gives up (default 1 << 20)
+  int force_err;         // diagnostics (SEPVAD_TCN_FORCE_GIVEUP): report a give-up without one happening
   int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
                          // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)

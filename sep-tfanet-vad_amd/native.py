@@ -46,6 +46,11 @@ class SepVadOutputs(ctypes.Structure):
 
 _lib = None
 
+# SEPVAD_CHECK=1: synchronise after every forward and raise if its fused TCN hand-offs gave up. Without it
+# a give-up (which needs the chip to be shared with work that starves the launch's groups for ~1 s) is
+# reported by the next forward on the same stream, or by Handle.fused_status().
+CHECK_EACH_FORWARD = os.environ.get("SEPVAD_CHECK", "0") not in ("", "0")
+
 
 def load_library(path: str = LIB_PATH):
     """Load libsepvad.so (after torch, so it binds to torch's HIP runtime) and declare signatures."""
@@ -250,6 +255,8 @@ class Handle:
         rc = self._lib.sepvad_forward_strided(self._h, _ptr(x), ldx, B, N, ctypes.byref(outs),
                                               ctypes.byref(kw) if kw is not None else None, self._stream())
         _check(rc, "sepvad_forward")
+        if CHECK_EACH_FORWARD:
+            self.fused_status()  # synchronises; raises if this forward's fused TCN gave up
         if vad is None:
             vad_ret = 0  # model/model.py:427
         elif kw is not None and kw.return_smoothed_vad:

@@ -25,10 +25,12 @@ _scratch = {}
 
 
 def _scratch_for(device):
-    buf = _scratch.get(device)
+    """Scratch of the current stream on `device` (one per stream: concurrent streams never share it)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    buf = _scratch.get(key)
     if buf is None:
         buf = torch.empty(PIT_SCRATCH_BYTES // 8, dtype=torch.float64, device=device)
-        _scratch[device] = buf
+        _scratch[key] = buf
     return buf
 
 

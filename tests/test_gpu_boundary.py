@@ -1,0 +1,145 @@
+"""The C-ABI contract of include/sepvad.h beyond parity (reference model/model.py:402-461):
+
+* concurrent forwards on different streams of ONE handle are allowed: each caller stream gets its own
+  workspace, hand-off words and give-up words, so two streams running at once give the same bits as a
+  serial run;
+* a fused-TCN hand-off give-up never passes as success: it is reported by the next forward on the same
+  stream (or by fused_status / SEPVAD_CHECK=1), is not sticky, and the forward after it is valid again;
+* a batch split over several persistent launches (launch salts, epoch counters) is bitwise equal to one;
+* the fp16 split of the GEMM operands keeps fp32-equivalent accuracy when weights or inputs are scaled
+  by 1e-3 or 1e3 (static power-of-two range scales, api.hip range_exp).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import config_of, load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SEP_TOL = 1e-4
+
+
+def _net(cfg, sd):
+    import sep_tfanet_vad_amd as pkg
+    net = pkg.SeparationModel(**cfg)
+    net.load_state_dict(sd, strict=True)
+    return net.eval().to(DEV)
+
+
+@pytest.fixture(scope="module")
+def net(state_dicts):
+    return _net(config_of("with_vad"), state_dicts["with_vad"])
+
+
+def test_two_streams_concurrently_match_serial(net):
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    x1 = torch.from_numpy(synth.make_batch(40, 32000, 11)[0]).to(DEV)
+    x2 = torch.from_numpy(synth.make_batch(24, 24000, 12)[0]).to(DEV)
+    with torch.no_grad():
+        r1 = h.forward(x1)
+        r2 = h.forward(x2)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):  # several rounds: the two streams' kernels overlap on the device
+        with torch.cuda.stream(s1):
+            a = h.forward(x1)
+        with torch.cuda.stream(s2):
+            b = h.forward(x2)
+        outs.append((a, b))
+    torch.cuda.synchronize()
+    assert h.fused_status()
+    for a, b in outs:
+        for k in ("sep", "vad", "est"):
+            assert torch.equal(a[k], r1[k]), k
+            assert torch.equal(b[k], r2[k]), k
+
+
+def test_giveup_is_reported_once_and_not_sticky(net):
+    g = load_golden("with_vad", "small")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    h = net.native_handle(DEV)
+    os.environ["SEPVAD_TCN_FORCE_GIVEUP"] = "1"
+    try:
+        h.forward(x)
+    finally:
+        del os.environ["SEPVAD_TCN_FORCE_GIVEUP"]
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="gave up"):
+        h.forward(x)  # the next forward on the same stream reports the earlier give-up
+    out = h.forward(x)  # reported once: this one is valid
+    assert h.fused_status()
+    assert np.abs(out["sep"].cpu().numpy() - g["sep"]).max() <= SEP_TOL
+    # and through fused_status (the synchronising check SEPVAD_CHECK=1 runs after every forward)
+    os.environ["SEPVAD_TCN_FORCE_GIVEUP"] = "1"
+    try:
+        h.forward(x)
+    finally:
+        del os.environ["SEPVAD_TCN_FORCE_GIVEUP"]
+    with pytest.raises(RuntimeError, match="gave up"):
+        h.fused_status()
+    assert h.fused_status()  # not sticky
+    out = h.forward(x)
+    assert np.abs(out["sep"].cpu().numpy() - g["sep"]).max() <= SEP_TOL
+
+
+def test_several_launches_per_forward_are_bitwise_identical(net):
+    """SEPVAD_TCN_MAX_ITER=1: every group handles one utterance per launch, so B=150 takes 3 launches
+    (new salt, offsets of S0 / Xfin / records per launch)."""
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(150, 32000, 4343)[0]).to(DEV)
+    h = net.native_handle(DEV)
+    a = {k: v.clone() for k, v in h.forward(x).items()}
+    os.environ["SEPVAD_TCN_MAX_ITER"] = "1"
+    try:
+        b = h.forward(x)
+        assert h.fused_status()
+    finally:
+        del os.environ["SEPVAD_TCN_MAX_ITER"]
+    for k in ("sep", "vad", "est"):
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("wscale", [1e-3, 1e3])
+def test_scaled_weights_keep_fp32_accuracy(wscale, state_dicts):
+    """Every weight except the STFT windows scaled by 1e-3 / 1e3: the fp16 planes would underflow
+    (subnormal) or overflow (inf) without the range scales. Gate: HIP (fp16x3) is as close to the fp64
+    oracle as the fp32 oracle is (x1e3 makes the problem itself ill-conditioned: the fp32 oracle is
+    6.5e-3 from fp64 there), and within 1e-4 where the problem is well conditioned."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    cfg = config_of("with_vad")
+    sd = {k: (v if k.endswith("window") else v * wscale) for k, v in state_dicts["with_vad"].items()}
+    x = torch.from_numpy(synth.make_batch(3, 32000, 77)[0])
+    net = _net(cfg, sd)
+    net.native_precision = "f16x3"
+    with torch.no_grad():
+        s, v, _ = net(x.to(DEV))
+    assert torch.isfinite(s).all() and torch.isfinite(v).all()
+    s32 = OracleModel(cfg, sd, torch.float32)(x)[0].double()
+    s64, v64, _ = OracleModel(cfg, sd, torch.float64)(x)
+    e32 = (s32 - s64).abs().max().item()
+    ehip = (s.cpu().double() - s64).abs().max().item()
+    assert ehip <= max(SEP_TOL, 3.0 * e32), (ehip, e32)
+    vr = v64.numpy()
+    safe = np.abs(vr - 0.5) > 1e-3
+    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+
+
+@pytest.mark.parametrize("xscale", [1e-3, 1e3])
+def test_scaled_inputs(xscale, net, state_dicts):
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(3, 32000, 78)[0]) * xscale
+    with torch.no_grad():
+        s, v, _ = net(x.to(DEV))
+    s_ref, v_ref, _ = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)(x)
+    assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL * max(1.0, xscale)
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])

@@ -69,3 +69,70 @@ def test_two_rank_gloo_shards_equal_single_process(tmp_path):
     ref = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float64)(torch.from_numpy(x))[0].numpy()
     assert sharded.shape == ref.shape
     assert np.abs(sharded - ref).max() <= 1e-12
+
+
+def _bench_worker(rank, world, port, n, out_dir):
+    """One rank of bench.py's own distributed path (init_dist / timed_region), gloo on CPU, with the
+    oracle as the model and shard_range as the utterance split."""
+    import sys
+    import types
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import bench
+    from oracle.torch_ref import OracleModel
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    from sep_tfanet_vad_amd.shard import shard_range
+    d, w, r, lr = bench.init_dist(types.SimpleNamespace(gpus=world), backend="gloo")
+    assert (w, r, lr) == (world, rank, rank) and d is not None
+    sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234).items()}
+    om = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float32)
+    x, _ = synth.make_batch(n, 4000, 901)
+    s, e = shard_range(n, rank, world)
+    xs = torch.from_numpy(x[s:e])
+    outs = []
+
+    def step():
+        outs.append(om(xs)[0])
+
+    el = bench.timed_region(step, 2, 1, d)
+    np.save(os.path.join(out_dir, f"sep{rank}.npy"), outs[-1].numpy())
+    np.save(os.path.join(out_dir, f"el{rank}.npy"), np.array([el, len(outs)]))
+    d.barrier()
+    d.destroy_process_group()
+
+
+def test_bench_distributed_path_gloo(tmp_path):
+    """bench.py's rank bookkeeping, barriers and max-over-ranks timing at world 2 (gloo): both ranks
+    report the same (max) elapsed time, each ran warmup + steps forwards, and the shards concatenate
+    to the single-process result."""
+    import sys
+    sys.path.insert(0, REPO)
+    from oracle.torch_ref import OracleModel
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    n = 3
+    mp.spawn(_bench_worker, args=(2, _free_port(), n, str(tmp_path)), nprocs=2, join=True)
+    e0, e1 = np.load(tmp_path / "el0.npy"), np.load(tmp_path / "el1.npy")
+    assert e0[0] == e1[0] > 0 and e0[1] == e1[1] == 3
+    sharded = np.concatenate([np.load(tmp_path / "sep0.npy"), np.load(tmp_path / "sep1.npy")])
+    sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234).items()}
+    x, _ = synth.make_batch(n, 4000, 901)
+    ref = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float32)(torch.from_numpy(x))[0].numpy()
+    assert np.abs(sharded - ref).max() <= 1e-6
+
+
+def test_bench_launcher_only_outside_torchrun(monkeypatch):
+    import sys
+    import types
+    sys.path.insert(0, REPO)
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.launch_ranks(types.SimpleNamespace(gpus=2)) is None   # already a torchrun rank
+    monkeypatch.delenv("WORLD_SIZE")
+    assert bench.launch_ranks(types.SimpleNamespace(gpus=1)) is None   # single GPU: in-process
+    with pytest.raises(SystemExit):
+        monkeypatch.setenv("WORLD_SIZE", "1")
+        bench.init_dist(types.SimpleNamespace(gpus=2))                  # world must equal --gpus
