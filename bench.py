@@ -52,17 +52,18 @@ def res_out_flops(B, T):
     return 2 * 256 * 512 * B * T
 
 
-def tcn_flops(B, T, nblk=24):
+def tcn_flops(B, T, precision="f16x3", nblk=24):
     """Algorithmic FLOPs of one fused-TCN launch: the two pointwise GEMMs of every block (SURVEY §8d,
     F_gemm without the output head): 24 * 2 * (256*256 + 512*256) per frame."""
     return nblk * 2 * (256 * 256 + 512 * 256) * B * T
 
 
-def tcn_bytes(B, T):
+def tcn_bytes(B, T, precision="f16x3"):
     """Compulsory HBM bytes of one fused-TCN launch: TCN input read + output written (fp32 [B][Tp][256]),
-    the fp16 hi/lo weights in fragment order (24 blocks x 768 KB) read once."""
+    the weights in fragment order read once (24 blocks x 768 KB as fp16 hi/lo, 384 KB as one 16-bit plane)."""
     Tp = (T + 63) // 64 * 64
-    return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * 4
+    wbytes = 4 if precision == "f16x3" else 2
+    return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * wbytes
 
 
 def res_out_bytes(B, T):
@@ -225,8 +226,9 @@ def main():
                     help="concurrent utterance chunks per forward (internal streams; bitwise-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
-                    help="GEMM arithmetic (both meet the fp32 parity gates; see DESIGN.md)")
+    ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32", "bf16", "f16"],
+                    help="GEMM arithmetic: f16x3 / fp32 meet the fp32 parity gates (default f16x3); bf16 / f16 are "
+                         "the reduced-precision arms (BASELINE cfg 2 / cfg 5; tolerance in DESIGN.md §4)")
     ap.add_argument("--workload", default="offline", choices=["offline", "stream"],
                     help="offline: cfg 2 (default, the BASELINE metric); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
@@ -286,11 +288,15 @@ def main():
         res_avg_s = res_ms / n_res / 1e3
         if fused:
             # dominant kernel = the fused persistent TCN (all 24 blocks in one launch)
-            flops_launch, bytes_launch = tcn_flops(B, T), tcn_bytes(B, T)
-            peak = F16_MFMA_PEAK_TFLOPS / 3.0
-            kern = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
-                    "512->256, TF-attention, recursive LN], fp16x3 split on v_mfma_f32_32x32x16_f16: peak = "
-                    "2.5 PF/s / 3)")
+            flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision)
+            body = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
+                    "512->256, TF-attention, recursive LN], ")
+            if args.precision == "f16x3":
+                peak = F16_MFMA_PEAK_TFLOPS / 3.0
+                kern = body + "fp16x3 split on v_mfma_f32_32x32x16_f16: peak = 2.5 PF/s / 3)"
+            else:
+                peak = F16_MFMA_PEAK_TFLOPS
+                kern = body + f"{args.precision} operands on v_mfma_f32_32x32x16_{args.precision}: peak = 2.5 PF/s)"
             pmc_name = PMC_FILE_FUSED
         else:
             flops_launch, bytes_launch = res_out_flops(B, T), res_out_bytes(B, T)
@@ -327,7 +333,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            # arithmetic type of the path: fp32 (fp16x3 is an fp32-equivalent split), or the reduced arm's operand
+            "dtype": {"f16x3": "fp32", "fp32": "fp32", "bf16": "bf16", "f16": "f16"}[args.precision],
             "gemm_arithmetic": args.precision,
             "split": args.split,
             "schedule": "fused" if fused else "multi-kernel",

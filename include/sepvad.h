@@ -37,11 +37,15 @@ enum {
 /* TCN residual mode (model/model.py:347-352). */
 enum { SEPVAD_LN_PLAIN = 0, SEPVAD_LN_RECURSIVE = 1, SEPVAD_LN_RESIDUAL = 2 };
 
-/* Arithmetic of the pointwise (1x1) GEMMs. Both meet the fp32 parity gates (max-abs <= 1e-4):
+/* Arithmetic of the pointwise (1x1) GEMMs (reference model/model.py:104,114,324). FP32 and F16X3 meet the
+ * fp32 parity gates (max-abs <= 1e-4):
  *   FP32:  v_mfma_f32_32x32x2_f32 (exact fp32 fma chain);
  *   F16X3: fp32-equivalent split: x = hi + lo (fp16 each), acc += hi*hi + hi*lo + lo*hi on
- *          v_mfma_f32_32x32x16_f16 with fp32 accumulation (default; 16x the fp32 MFMA rate per pass). */
-enum { SEPVAD_PREC_FP32 = 0, SEPVAD_PREC_F16X3 = 1 };
+ *          v_mfma_f32_32x32x16_f16 with fp32 accumulation (default; 16x the fp32 MFMA rate per pass).
+ * F16 and BF16 are the reduced-precision arms (BASELINE cfg 2 "bf16", cfg 5 "fp16 vs fp32"): operands
+ * rounded to fp16 / bf16, one v_mfma_f32_32x32x16_{f16,bf16} product, fp32 accumulation; everything outside
+ * the GEMMs stays fp32. Their tolerance vs fp32 is measured, not gated. */
+enum { SEPVAD_PREC_FP32 = 0, SEPVAD_PREC_F16X3 = 1, SEPVAD_PREC_F16 = 2, SEPVAD_PREC_BF16 = 3 };
 
 /* SeparationModel kwargs that change the computation (model/model.py:362-366). */
 typedef struct SepVadConfig {
@@ -114,7 +118,7 @@ int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int
 int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit);
 
 /* Select the TCN schedule of later forwards: 1 (default, or env SEPVAD_FUSED) = the whole separator stack
- * as one persistent launch when the GEMMs are F16X3 and T <= 256 (groups of ceil(T/32) workgroups per
+ * as one persistent launch when the GEMMs are F16X3 / F16 / BF16 and T <= 256 (groups of ceil(T/32) workgroups per
  * utterance); 0 = one launch per stage (4 per block). Both meet the same parity gates. */
 int32_t sepvad_set_fused(sepvad_handle h, int32_t on);
 /* Synchronises the device and reports the schedule of the last forward and the persistent launch's

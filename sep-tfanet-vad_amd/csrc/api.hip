@@ -46,6 +46,7 @@ int fail(int code, const std::string& msg) {
 struct PackedW {
   size_t w32 = 0, whi = 0, wlo = 0, scale = 0;
   size_t fhi = 0, flo = 0;  // fused-TCN copies in MFMA B-fragment order (see pack_pointwise)
+  size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
 };
 
 struct BlockOff {
@@ -132,8 +133,11 @@ struct sepvad_model {
   hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
   // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs run fp16x3 and T <= 256
   bool fused = true;
-  int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU)
-  __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered weights
+  int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU), max over precisions
+  int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
+  __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered fp16 hi/lo weights (F16X3)
+  __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
+  __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
@@ -205,13 +209,24 @@ std::vector<float> fold_wn(const float* g, const float* v, int cout, int rest) {
   return w;
 }
 
+// float -> bf16 bits, round to nearest even (finite inputs: weights)
+__half bf16_bits(float f) {
+  unsigned u;
+  std::memcpy(&u, &f, 4);
+  u = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+  const unsigned short b = (unsigned short)u;
+  __half h;
+  std::memcpy(&h, &b, 2);
+  return h;
+}
+
 // [cout][cin] fp32 -> zero-padded [mpad][cin] fp32 + the fp16 hi/lo split of each row scaled by
 // 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^(e + col_e) undoes it exactly, and
 // also the 2^-col_e the GEMM applies to its A operand before splitting it (range guard, see range_exp).
 PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int cin, int mpad, int col_e = 0) {
   PackedW p;
   std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
-  std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin);
+  std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin), bf((size_t)mpad * cin);
   for (int o = 0; o < mpad; ++o) {
     float mx = 0.f;
     if (o < cout)
@@ -227,17 +242,19 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
       const __half hh = __float2half_rn(vs);
       hi[(size_t)o * cin + i] = hh;
       lo[(size_t)o * cin + i] = __float2half_rn(vs - __half2float(hh));
+      bf[(size_t)o * cin + i] = bf16_bits(vs);
     }
   }
   p.w32 = pk.add(w32);
   p.scale = pk.add(sc);
   p.whi = pk.addh(hi);
   p.wlo = pk.addh(lo);
+  p.wbf = pk.addh(bf);
   // k_tcn streams each wave's 32 output rows as consecutive 1 KB fragments (v_mfma_f32_32x32x16_f16
   // B operand): [mpad/32 row tiles][cin/16 K steps][64 lanes][8 halves], lane l -> row 32*mt + (l & 31),
   // k = 16*s + 8*(l >> 5) + j.
   if (mpad % 32 == 0 && cin % 16 == 0) {
-    std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin);
+    std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin), fb((size_t)mpad * cin);
     size_t q = 0;
     for (int mt = 0; mt < mpad / 32; ++mt)
       for (int st = 0; st < cin / 16; ++st)
@@ -246,9 +263,11 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
             const size_t src = (size_t)(32 * mt + (l & 31)) * cin + 16 * st + 8 * (l >> 5) + j;
             fh[q] = hi[src];
             fl[q] = lo[src];
+            fb[q] = bf[src];
           }
     p.fhi = pk.addh(fh);
     p.flo = pk.addh(fl);
+    p.fbf = pk.addh(fb);
   }
   return p;
 }
@@ -336,6 +355,7 @@ void set_weights(const sepvad_model* h, GemmArgs& g, const PackedW& w) {
   g.W32 = h->P(w.w32);
   g.Whi = h->H(w.whi);
   g.Wlo = h->H(w.wlo);
+  g.Wbf = h->H(w.wbf);
   g.wscale = h->P(w.scale);
 }
 
@@ -373,9 +393,12 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int ln = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
-  h->tcn_cap = ncu * tcn_blocks_per_cu(ln);
+  for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
+    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p);
+    h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
+  }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
-  std::vector<__half> wf(WF_BLOCK * h->nblk);
+  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
   for (int i = 0; i < h->nblk; ++i) {
@@ -385,6 +408,10 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     std::copy_n(pk.hblob.begin() + bo.w1.flo, WF_W1L, w + WF_W1L);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WF_W2L - WF_W2H, w + WF_W2H);
     std::copy_n(pk.hblob.begin() + bo.w2.flo, WF_W2L - WF_W2H, w + WF_W2L);
+    std::copy_n(pk.hblob.begin() + bo.w1.fhi, WS_W2, ws16.data() + WS_BLOCK * i);
+    std::copy_n(pk.hblob.begin() + bo.w2.fhi, WS_BLOCK - WS_W2, ws16.data() + WS_BLOCK * i + WS_W2);
+    std::copy_n(pk.hblob.begin() + bo.w1.fbf, WS_W2, wsbf.data() + WS_BLOCK * i);
+    std::copy_n(pk.hblob.begin() + bo.w2.fbf, WS_BLOCK - WS_W2, wsbf.data() + WS_BLOCK * i + WS_W2);
     float* q = pb.data() + (size_t)PB_SIZE * i;
     auto put = [&](int off, size_t src, int n) { std::copy_n(pk.blob.begin() + src, n, q + off); };
     put(PB_WS1, bo.w1.scale, CH); put(PB_B1, bo.b1, CH); put(PB_G1, bo.g1, CH); put(PB_BE1, bo.be1, CH);
@@ -403,6 +430,10 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   }
   HIPCHK(hipMalloc(&h->twf, wf.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twf16, ws16.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twf16, ws16.data(), ws16.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twbf, wsbf.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twbf, wsbf.data(), wsbf.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->tprm, pb.size() * sizeof(float)));
   HIPCHK(hipMemcpy(h->tprm, pb.data(), pb.size() * sizeof(float), hipMemcpyHostToDevice));
   return SEPVAD_OK;
@@ -465,7 +496,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
   if (!cfg || !tensors || !names || !numels) { g_err = "null argument"; return nullptr; }
   const SepVadConfig& c = *cfg;
   if (c.n_fft != NFFT || c.bn_dim != CH || c.h_dim != HID || c.num_spk != 2 || c.layer < 1 || c.stack < 1 ||
-      (c.precision != SEPVAD_PREC_FP32 && c.precision != SEPVAD_PREC_F16X3)) {
+      c.precision < SEPVAD_PREC_FP32 || c.precision > SEPVAD_PREC_BF16) {
     g_err = "unsupported configuration (native path: n_fft=512, BN_dim=256, H_dim=512, num_spk=2)";
     return nullptr;
   }
@@ -478,7 +509,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
   h->cfg = c;
   h->device = device;
   h->nblk = c.layer * c.stack;
-  h->prec = c.precision == SEPVAD_PREC_FP32 ? PREC_F32 : PREC_F16X3;
+  h->prec = c.precision;  // SEPVAD_PREC_* == PREC_* (static_asserts below)
   Packer pk;
   bool ok = true;
   auto get = [&](const std::string& k, int64_t numel) -> const float* {
@@ -720,9 +751,8 @@ int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N) {
 
 int32_t sepvad_set_precision(sepvad_handle h, int32_t precision) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
-  if (precision == SEPVAD_PREC_FP32) h->prec = PREC_F32;
-  else if (precision == SEPVAD_PREC_F16X3) h->prec = PREC_F16X3;
-  else return fail(SEPVAD_E_ARG, "unknown precision");
+  if (precision < SEPVAD_PREC_FP32 || precision > SEPVAD_PREC_BF16) return fail(SEPVAD_E_ARG, "unknown precision");
+  h->prec = precision;
   return SEPVAD_OK;
 }
 
@@ -746,9 +776,12 @@ namespace {
 
 // The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 256) and a group fits
 // the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
+static_assert(SEPVAD_PREC_FP32 == PREC_F32 && SEPVAD_PREC_F16X3 == PREC_F16X3 && SEPVAD_PREC_F16 == PREC_F16 &&
+              SEPVAD_PREC_BF16 == PREC_BF16, "precision codes");
+
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec == PREC_F16X3 && G <= FG_MAX && h->tcn_cap >= G;
+  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && h->tcn_cap_p[h->prec] >= G;
 }
 
 int env_int(const char* name, int dflt) {
@@ -809,13 +842,15 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.T = T; ta.Tp = Tp; ta.G = G; ta.nblk = h->nblk; ta.layer = c.layer;
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
-    ta.wfrag = h->twf; ta.prm = h->tprm;
+    ta.prec = h->prec;
+    ta.wfrag = h->prec == PREC_F16X3 ? h->twf : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
+    ta.prm = h->tprm;
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
-    int ngroups = std::min(B, h->tcn_cap / G);
+    int ngroups = std::min(B, h->tcn_cap_p[h->prec] / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + 4 per block per utterance, < 2^TCN_EPOCH_BITS
     // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)
@@ -918,7 +953,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       g2.B = B; g2.T = T; g2.Tp = Tp; g2.M = CH; g2.Mreal = CH; g2.K = HID; g2.ldy = CH;
       set_weights(h, g2, bo.w2);
       g2.bias = h->P(bo.b2);
-      if (h->prec == PREC_F16X3) {
+      if (h->prec != PREC_F32) {
         g2.ld.mode = LD_SPLIT; g2.ld.Xh = w.Dhi; g2.ld.Xl = w.Dlo;
       } else {
         g2.ld.mode = LD_PLAIN; g2.ld.X = w.D32;
@@ -1244,6 +1279,8 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->fork) (void)hipEventDestroy(h->fork);
   for (auto& c : h->ctx) free_ctx(c.release());
   if (h->twf) (void)hipFree(h->twf);
+  if (h->twf16) (void)hipFree(h->twf16);
+  if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
   if (h->dparams) (void)hipFree(h->dparams);

@@ -40,6 +40,7 @@
 namespace sepvad {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
@@ -145,39 +146,58 @@ constexpr int GW_ROW = 0;           // P3: per-channel sums over own frames [256
 constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
 static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
+// Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
+template <int PRE>
+struct WLay {
+  static constexpr size_t BLOCK = PRE == PREC_F16X3 ? WF_BLOCK : WS_BLOCK;
+  static constexpr size_t W1H = 0, W1L = PRE == PREC_F16X3 ? WF_W1L : 0;
+  static constexpr size_t W2H = PRE == PREC_F16X3 ? WF_W2H : WS_W2, W2L = PRE == PREC_F16X3 ? WF_W2L : 0;
+};
+
 // conv1d / res_out GEMM of one wave: acc[32 frames x 32 channels] += A[32 x 16*NS] * W^T. A comes from
 // LDS (hi/lo planes, row stride LDA); the W fragments stream from global (buffer loads over the
 // fragment-ordered weight, this lane's bytes at voff + 1024 * step) with PD steps in flight in a
 // static register ring; the first PD steps are already in (rh, rl) on entry.
-template <int NS, int LDA>
+// PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
+// hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
+template <int NS, int LDA, int PRE>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
                                           u32x4v (&rh)[PD], u32x4v (&rl)[PD], int lane) {
   static_assert(NS % PD == 0 && NS > PD, "K steps");
+  constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
   // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
   f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff);
-  f16x8 al = *reinterpret_cast<const f16x8*>(Alo + aoff);
+  f16x8 al = ah;
+  if constexpr (X3) al = *reinterpret_cast<const f16x8*>(Alo + aoff);
   auto step = [&](int s, int i, bool pf) {
     f16x8 nh = ah, nl = al;
     if (s + 1 < NS) {
       nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
-      nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
+      if constexpr (X3) nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
     }
-    const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
-    const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+    if constexpr (X3) {
+      const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
+      const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+    } else if constexpr (PRE == PREC_F16) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, __builtin_bit_cast(f16x8, rh[i]), acc, 0, 0, 0);
+    } else {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, rh[i]),
+                                                    acc, 0, 0, 0);
+    }
     if (pf) {
       rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + PD) * 1024, 0);
-      rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + PD) * 1024, 0);
+      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + PD) * 1024, 0);
     }
     ah = nh; al = nl;
-    // pipeline shape of a step: next step's A reads (DS), this step's 3 MFMAs, then the ring refill (VMEM)
-    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+    // pipeline shape of a step: next step's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 : 1, 0);
+    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, X3 ? 2 : 1, 0);
     // keep program order per step: the scheduler otherwise may sink the refill loads to their use and
     // collapse the ring to one step in flight (seen as s_waitcnt vmcnt(1) before every step)
     __builtin_amdgcn_sched_barrier(0);
@@ -191,27 +211,45 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   for (int i = 0; i < PD; ++i) step(NS - PD + i, i, false);
 }
 
+template <int PRE>
 __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
                                            u32x4v (&rh)[PD], u32x4v (&rl)[PD]) {
 #pragma unroll
   for (int s = 0; s < PD; ++s) {
     rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
-    rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+    if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
   }
 }
 
+// One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
+// bf16 bits (BF16, round to nearest even) in the hi plane.
+template <int PRE>
 __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, int idx, float v) {
-  const _Float16 h = (_Float16)v;
-  hi[idx] = h;
-  lo[idx] = (_Float16)(v - (float)h);
+  if constexpr (PRE == PREC_F16X3) {
+    const _Float16 h = (_Float16)v;
+    hi[idx] = h;
+    lo[idx] = (_Float16)(v - (float)h);
+  } else if constexpr (PRE == PREC_F16) {
+    hi[idx] = (_Float16)v;
+  } else {
+    reinterpret_cast<__bf16*>(hi)[idx] = (__bf16)v;
+  }
 }
 
 // two adjacent values (idx even): one 32-bit LDS store per plane
+template <int PRE>
 __device__ __forceinline__ void split_store2(_Float16* hi, _Float16* lo, int idx, float v0, float v1) {
   typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-  const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
-  *reinterpret_cast<f16x2*>(hi + idx) = f16x2{h0, h1};
-  *reinterpret_cast<f16x2*>(lo + idx) = f16x2{(_Float16)(v0 - (float)h0), (_Float16)(v1 - (float)h1)};
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  if constexpr (PRE == PREC_F16X3) {
+    const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+    *reinterpret_cast<f16x2*>(hi + idx) = f16x2{h0, h1};
+    *reinterpret_cast<f16x2*>(lo + idx) = f16x2{(_Float16)(v0 - (float)h0), (_Float16)(v1 - (float)h1)};
+  } else if constexpr (PRE == PREC_F16) {
+    *reinterpret_cast<f16x2*>(hi + idx) = f16x2{(_Float16)v0, (_Float16)v1};
+  } else {
+    *reinterpret_cast<bf16x2*>(hi + idx) = bf16x2{(__bf16)v0, (__bf16)v1};
+  }
 }
 
 // GroupNorm affine of the 256 channels, one per thread tid < CH (as device_common.h gn_affine); the
@@ -315,8 +353,9 @@ __device__ __forceinline__ KArgs kargs() {
   return p;
 }
 
-template <int LM>
+template <int LM, int PRE>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
+  using WL = WLay<PRE>;
   __shared__ __attribute__((aligned(16))) TcnSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
@@ -378,7 +417,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const KArgs ka = kargs();
       const __amdgpu_buffer_rsrc_t s0r = rsrc_of(ka->S0 + ((size_t)u * Tp + t0) * CH);
       const __amdgpu_buffer_rsrc_t gr = rsrc_of(ka->ln.g), ber = rsrc_of(ka->ln.be);
-      const __amdgpu_buffer_rsrc_t w1h = rsrc_of(ka->wfrag), w1l = rsrc_of(ka->wfrag + WF_W1L);
+      const __amdgpu_buffer_rsrc_t w1h = rsrc_of(ka->wfrag), w1l = rsrc_of(ka->wfrag + WL::W1L);
       const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
       const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * 16;
       __builtin_amdgcn_sched_barrier(0);
@@ -390,7 +429,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
       sx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc_of(ka->prm), 0, PB_SX * 4, 0));
-      prefetch_w(w1h, w1l, voffu, rh, rl);  // block-0 conv1d weights: in flight with the input rows
+      prefetch_w<PRE>(w1h, w1l, voffu, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
     if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
@@ -429,7 +468,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int tl = trow(r);
         o[r] = fmaf(raw[r], s, h) * (t0 + tl < T ? 1.f : 0.f);
-        split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
+        split_store<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
       }
     }
     __syncthreads();
@@ -446,7 +485,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(0);
       if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
         a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
-      const __half* wb = a.wfrag + (size_t)bi * WF_BLOCK;
+      const __half* wb = a.wfrag + (size_t)bi * WL::BLOCK;
       const int li = bi % a.layer;
       const int dil = li == 0 ? 1 : (li % 4 + 1);   // model/model.py:285-295 (as api.hip packs it)
       const float* pm = sm.prm;
@@ -467,7 +506,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS1, LDX>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WF_W1L), voff1, rh, rl, lane);
+        wave_gemm<NS1, LDX, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, rh, rl, lane);
       TPROBE(1);
       }
       {
@@ -526,7 +565,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         if (sk >= 0) sm.gw[sk] = v[4];
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        prefetch_w(rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl);
+        prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
@@ -580,7 +619,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               st[0] += v; st[1] += v * v;
               dv[q] = v;
             }
-            split_store2(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
+            split_store2<PRE>(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
           }
         };
         switch (dil) {
@@ -599,7 +638,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS2, LDD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WF_W2H), rsrc_of(wb + WF_W2L), voff2, rh, rl, lane);
+        wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
       {
@@ -770,8 +809,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       // next block's conv1d weights: in flight during the x' update
       if (bi + 1 < a.nblk) {
-        const __half* wn = wb + WF_BLOCK;
-        prefetch_w(rsrc_of(wn), rsrc_of(wn + WF_W1L), voff1, rh, rl);
+        const __half* wn = wb + WL::BLOCK;
+        prefetch_w<PRE>(rsrc_of(wn), rsrc_of(wn + WL::W1L), voff1, rh, rl);
       }
       TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
@@ -782,7 +821,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
-          split_store(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sxn);
+          split_store<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sxn);
         }
       }
       __syncthreads();
@@ -810,27 +849,47 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   }
 }
 
-hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
-  if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || grid < a.G || grid % a.G)
-    return hipErrorInvalidValue;
+template <int PRE>
+static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
   switch (a.ln_mode) {
-    case LD_RECURSIVE: hipLaunchKernelGGL(k_tcn<LD_RECURSIVE>, dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_RESIDUAL: hipLaunchKernelGGL(k_tcn<LD_RESIDUAL>, dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_ADD: hipLaunchKernelGGL(k_tcn<LD_ADD>, dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-int tcn_blocks_per_cu(int ln_mode) {
+hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
+  if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || grid < a.G || grid % a.G)
+    return hipErrorInvalidValue;
+  switch (a.prec) {
+    case PREC_F16X3: return launch_tcn_pre<PREC_F16X3>(a, grid, s);
+    case PREC_F16: return launch_tcn_pre<PREC_F16>(a, grid, s);
+    case PREC_BF16: return launch_tcn_pre<PREC_BF16>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int PRE>
+static int blocks_per_cu_pre(int ln_mode) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
   switch (ln_mode) {
-    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE>, NTHR, 0); break;
-    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL>, NTHR, 0); break;
-    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD>, NTHR, 0); break;
+    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE, PRE>, NTHR, 0); break;
+    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE>, NTHR, 0); break;
+    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE>, NTHR, 0); break;
   }
   return e == hipSuccess ? nb : 0;
+}
+
+int tcn_blocks_per_cu(int ln_mode, int prec) {
+  switch (prec) {
+    case PREC_F16X3: return blocks_per_cu_pre<PREC_F16X3>(ln_mode);
+    case PREC_F16: return blocks_per_cu_pre<PREC_F16>(ln_mode);
+    case PREC_BF16: return blocks_per_cu_pre<PREC_BF16>(ln_mode);
+  }
+  return 0;
 }
 
 }  // namespace sepvad

@@ -18,6 +18,8 @@
 //               Products of fp16 are exact in fp32, so only the dropped lo*lo term (~2^-22 relative)
 //               and fp32 accumulation remain: parity matches the fp32 path (tests/test_gpu_parity.py).
 //   PREC_F32:   v_mfma_f32_32x32x2_f32 (exact fp32 fma chain), 1/16 of the f16 MFMA rate.
+//   PREC_F16 / PREC_BF16: reduced-precision arms, one v_mfma_f32_32x32x16_{f16,bf16} per 16-deep step on the
+//               hi plane only (operands rounded to fp16 / bf16, fp32 accumulation).
 // Tile 64 frames x 64 channels, K chunk 64, 4 waves (2x2), one 32x32 accumulator per wave;
 // single-buffered LDS fed from two register sets: chunk k+1 waits in registers to be staged while
 // chunk k+2 is in flight during chunk k's MFMAs.
@@ -26,6 +28,7 @@
 namespace sepvad {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP's uint4 wrapper can defeat SROA)
 
@@ -61,8 +64,10 @@ __device__ __forceinline__ void split4(const float4& v, uint2& hi, uint2& lo) {
 
 template <int PREC, int LM, int HEAD, int EP>
 __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
-  static_assert(LM != LD_SPLIT || PREC == PREC_F16X3, "pre-split operands are fp16x3 only");
-  using Smem = typename std::conditional<PREC == PREC_F16X3, SmemF16, SmemF32>::type;
+  static_assert(LM != LD_SPLIT || PREC != PREC_F32, "pre-split operands are 16-bit planes");
+  constexpr bool H16 = PREC != PREC_F32;     // 16-bit operand planes in LDS
+  constexpr bool X3 = PREC == PREC_F16X3;    // ... with a lo plane
+  using Smem = typename std::conditional<H16, SmemF16, SmemF32>::type;
   __shared__ __attribute__((aligned(16))) Smem sm;
   constexpr bool NEED_C = (LM == LD_GN || LM == LD_RECURSIVE || LM == LD_RESIDUAL);
   constexpr bool GATED = (LM == LD_RECURSIVE || LM == LD_RESIDUAL || LM == LD_ADD);
@@ -104,8 +109,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
       const size_t o0 = (arow0 + hrow) * K + k0 + 8 * hq, o1 = o0 + (size_t)32 * K;
       q.ah0 = *reinterpret_cast<const u32x4*>(ld.Xh + o0);
       q.ah1 = *reinterpret_cast<const u32x4*>(ld.Xh + o1);
-      q.al0 = *reinterpret_cast<const u32x4*>(ld.Xl + o0);
-      q.al1 = *reinterpret_cast<const u32x4*>(ld.Xl + o1);
+      if constexpr (X3) {
+        q.al0 = *reinterpret_cast<const u32x4*>(ld.Xl + o0);
+        q.al1 = *reinterpret_cast<const u32x4*>(ld.Xl + o1);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -116,12 +123,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
         if constexpr (GATED) q.rr[i] = *reinterpret_cast<const float4*>(ld.X2 + off);
       }
     }
-    if constexpr (PREC == PREC_F16X3) {
+    if constexpr (H16) {
       const size_t o0 = (size_t)(m0 + hrow) * K + k0 + 8 * hq, o1 = o0 + (size_t)32 * K;
-      q.wh0 = *reinterpret_cast<const u32x4*>(a.Whi + o0);
-      q.wh1 = *reinterpret_cast<const u32x4*>(a.Whi + o1);
-      q.wl0 = *reinterpret_cast<const u32x4*>(a.Wlo + o0);
-      q.wl1 = *reinterpret_cast<const u32x4*>(a.Wlo + o1);
+      const __half* wp = PREC == PREC_BF16 ? a.Wbf : a.Whi;
+      q.wh0 = *reinterpret_cast<const u32x4*>(wp + o0);
+      q.wh1 = *reinterpret_cast<const u32x4*>(wp + o1);
+      if constexpr (X3) {
+        q.wl0 = *reinterpret_cast<const u32x4*>(a.Wlo + o0);
+        q.wl1 = *reinterpret_cast<const u32x4*>(a.Wlo + o1);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NWF; ++i) {
@@ -139,6 +149,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
       split4(make_float4(v.x * s, v.y * s, v.z * s, v.w * s), hi, lo);
       *reinterpret_cast<uint2*>(&sm.Ahi[row][col]) = hi;
       *reinterpret_cast<uint2*>(&sm.Alo[row][col]) = lo;
+    } else if constexpr (PREC == PREC_F16) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const float s = a.ascale;
+      *reinterpret_cast<h4*>(&sm.Ahi[row][col]) = h4{(_Float16)(v.x * s), (_Float16)(v.y * s), (_Float16)(v.z * s),
+                                                      (_Float16)(v.w * s)};
+    } else if constexpr (PREC == PREC_BF16) {
+      typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+      const float s = a.ascale;  // bf16 has the fp32 range, but wscale carries the inverse of the scale
+      *reinterpret_cast<b4*>(&sm.Ahi[row][col]) = b4{(__bf16)(v.x * s), (__bf16)(v.y * s), (__bf16)(v.z * s),
+                                                     (__bf16)(v.w * s)};
     } else {
       sm.A[row][col + 0] = v.x; sm.A[row][col + 1] = v.y;
       sm.A[row][col + 2] = v.z; sm.A[row][col + 3] = v.w;
@@ -154,8 +174,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
     if constexpr (LM == LD_SPLIT) {
       *reinterpret_cast<u32x4*>(&sm.Ahi[hrow][8 * hq]) = q.ah0;
       *reinterpret_cast<u32x4*>(&sm.Ahi[hrow + 32][8 * hq]) = q.ah1;
-      *reinterpret_cast<u32x4*>(&sm.Alo[hrow][8 * hq]) = q.al0;
-      *reinterpret_cast<u32x4*>(&sm.Alo[hrow + 32][8 * hq]) = q.al1;
+      if constexpr (X3) {
+        *reinterpret_cast<u32x4*>(&sm.Alo[hrow][8 * hq]) = q.al0;
+        *reinterpret_cast<u32x4*>(&sm.Alo[hrow + 32][8 * hq]) = q.al1;
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -185,11 +207,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
         put_a(row, c4, v);
       }
     }
-    if constexpr (PREC == PREC_F16X3) {
+    if constexpr (H16) {
       *reinterpret_cast<u32x4*>(&sm.Bhi[hrow][8 * hq]) = q.wh0;
       *reinterpret_cast<u32x4*>(&sm.Bhi[hrow + 32][8 * hq]) = q.wh1;
-      *reinterpret_cast<u32x4*>(&sm.Blo[hrow][8 * hq]) = q.wl0;
-      *reinterpret_cast<u32x4*>(&sm.Blo[hrow + 32][8 * hq]) = q.wl1;
+      if constexpr (X3) {
+        *reinterpret_cast<u32x4*>(&sm.Blo[hrow][8 * hq]) = q.wl0;
+        *reinterpret_cast<u32x4*>(&sm.Blo[hrow + 32][8 * hq]) = q.wl1;
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NWF; ++i) {
@@ -252,7 +276,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   probe(1);
 
   auto mma = [&]() {
-    if constexpr (PREC == PREC_F16X3) {
+    if constexpr (PREC == PREC_F16 || PREC == PREC_BF16) {
+      const int ar = wr * 32 + (lane & 31), br = wc * 32 + (lane & 31), kh = 8 * (lane >> 5);
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        const half8 ah = *reinterpret_cast<const half8*>(&sm.Ahi[ar][16 * s + kh]);
+        const half8 bh = *reinterpret_cast<const half8*>(&sm.Bhi[br][16 * s + kh]);
+        if constexpr (PREC == PREC_F16)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+        else
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah), __builtin_bit_cast(bf8, bh), acc,
+                                                        0, 0, 0);
+      }
+    } else if constexpr (PREC == PREC_F16X3) {
       const int ar = wr * 32 + (lane & 31), br = wc * 32 + (lane & 31), kh = 8 * (lane >> 5);
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
@@ -298,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs a) {
   // (the loop's last barrier guarantees every wave is done reading `sm`: it is reused below)
   const int col = lane & 31, half = lane >> 5;
   const int ml = wc * 32 + col, m = m0 + ml;
-  const float ws = (PREC == PREC_F16X3) ? a.wscale[m] : 1.f;
+  const float ws = H16 ? a.wscale[m] : 1.f;
   const float bias = a.bias[m];
   auto tloc = [&](int r) { return wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * half; };
 
@@ -428,7 +464,7 @@ static hipError_t dispatch_ld(const GemmArgs& a, dim3 grid, hipStream_t s) {
     if (lm == LD_PLAIN) {
       hipLaunchKernelGGL((k_gemm<PREC, LD_PLAIN, 0, EP>), grid, block, 0, s, a);
     } else if (lm == LD_SPLIT) {
-      if constexpr (PREC == PREC_F16X3) hipLaunchKernelGGL((k_gemm<PREC, LD_SPLIT, 0, EP>), grid, block, 0, s, a);
+      if constexpr (PREC != PREC_F32) hipLaunchKernelGGL((k_gemm<PREC, LD_SPLIT, 0, EP>), grid, block, 0, s, a);
       else return hipErrorInvalidValue;
     } else {
       return hipErrorInvalidValue;
@@ -452,7 +488,11 @@ static hipError_t dispatch_ep(const GemmArgs& a, int ep, dim3 grid, hipStream_t 
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s) {
   if (a.M % BMC || a.K % (2 * BK) || a.Tp % BT || a.K > KMAX) return hipErrorInvalidValue;
   const dim3 grid(a.B * (a.Tp / BT), a.M / BMC);
-  if (a.prec == PREC_F16X3) return dispatch_ep<PREC_F16X3>(a, ep, grid, s);
+  switch (a.prec) {
+    case PREC_F16X3: return dispatch_ep<PREC_F16X3>(a, ep, grid, s);
+    case PREC_F16: return dispatch_ep<PREC_F16>(a, ep, grid, s);
+    case PREC_BF16: return dispatch_ep<PREC_BF16>(a, ep, grid, s);
+  }
   return dispatch_ep<PREC_F32>(a, ep, grid, s);
 }
 

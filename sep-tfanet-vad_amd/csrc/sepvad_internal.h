@@ -28,7 +28,9 @@ constexpr int NMOM = 11;        // moment record of k_att_stats (see device_comm
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
-enum Precision { PREC_F32 = 0, PREC_F16X3 = 1 };
+// GEMM arithmetic. F32 and F16X3 are fp32-equivalent (parity path); F16 and BF16 are the reduced-
+// precision arms (one fp16 / bf16 product per MAC, fp32 accumulation; BASELINE cfg 2 bf16, cfg 5 fp16).
+enum Precision { PREC_F32 = 0, PREC_F16X3 = 1, PREC_F16 = 2, PREC_BF16 = 3 };
 
 // Residual-stream transform applied to the GEMM A operand as it is staged (normalize-on-load).
 enum LoadMode {
@@ -75,7 +77,8 @@ struct GemmArgs {
   int B, T, Tp, M, Mreal, K, ldy;
   int prec;
   const float* W32;                        // [M][K] fp32 (PREC_F32)
-  const __half* Whi; const __half* Wlo;    // [M][K] fp16 split of (w * 2^-e_m)  (PREC_F16X3)
+  const __half* Whi; const __half* Wlo;    // [M][K] fp16 split of (w * 2^-e_m)  (PREC_F16X3; F16 uses Whi)
+  const __half* Wbf;                       // [M][K] bf16 bits of (w * 2^-e_m)  (PREC_BF16)
   const float* wscale;                     // [M] 2^e_m (F16X3)
   const float* bias;                       // [M]
   float prelu;
@@ -244,9 +247,11 @@ constexpr int PB_EPS2 = 4898;                                      // reg2 eps, 
 constexpr int PB_SIZE = 4900;                                      // multiple of 4 (float4 staging)
 // fp16 hi/lo weights of one block in MFMA fragment order: conv1d hi | lo (256x256) | res_out hi | lo (256x512)
 constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
+// single-plane (PREC_F16 / PREC_BF16) blobs: conv1d (256x256) | res_out (256x512)
+constexpr size_t WS_W2 = 65536, WS_BLOCK = 196608;  // halves
 struct TcnArgs {
-  int B, T, Tp, G, nblk, layer, ln_mode, tf_att;
-  const __half* wfrag;   // [nblk][WF_BLOCK] fragment-ordered weights
+  int B, T, Tp, G, nblk, layer, ln_mode, tf_att, prec;
+  const __half* wfrag;   // [nblk][WF_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
   const float* prm;      // [nblk][PB_SIZE] parameter blobs
   const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
   GnSrc ln;              // TCN.LN statistics records (k_gate) + affine
@@ -264,7 +269,7 @@ struct TcnArgs {
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
-int tcn_blocks_per_cu(int ln_mode);
+int tcn_blocks_per_cu(int ln_mode, int prec);
 
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);

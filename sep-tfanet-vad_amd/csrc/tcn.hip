@@ -3,7 +3,7 @@
 //                 (model/model.py:414-419); writes the TCN input (bins 1..256); TCN.LN statistics
 //                 (model/model.py:333,421) records
 //   k_dw_stats    d = PReLU(dconv(GN1(a))) (model/model.py:132-135), written once as the res_out
-//                 GEMM operand (fp16 hi/lo split for PREC_F16X3), and its statistics for reg2
+//                 GEMM operand (fp16 hi/lo split for PREC_F16X3, one fp16 / bf16 plane for F16 / BF16), and its statistics for reg2
 //                 (model/model.py:136), which the res_out epilogue folds in
 //   k_att_stats   TF_Attention gates a_t, a_f (model/model.py:197-205) from the res_out epilogue's partial
 //                 means, and the moment records of the residual update (model/model.py:345-350)
@@ -124,6 +124,11 @@ __global__ __launch_bounds__(256) void k_dw_stats(DwStatsArgs a) {
       const __half l0 = __float2half_rn(v[0] - __half2float(h0)), l1 = __float2half_rn(v[1] - __half2float(h1v));
       *reinterpret_cast<__half2*>(a.Dhi + off) = __halves2half2(h0, h1v);
       *reinterpret_cast<__half2*>(a.Dlo + off) = __halves2half2(l0, l1);
+    } else if (a.prec == PREC_F16) {
+      *reinterpret_cast<__half2*>(a.Dhi + off) = __halves2half2(__float2half_rn(v[0]), __float2half_rn(v[1]));
+    } else if (a.prec == PREC_BF16) {
+      typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<b2*>(a.Dhi + off) = b2{(__bf16)v[0], (__bf16)v[1]};
     } else {
       *reinterpret_cast<float2*>(a.D32 + off) = make_float2(v[0], v[1]);
     }

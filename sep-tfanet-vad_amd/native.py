@@ -16,8 +16,9 @@ import torch
 LIB_PATH = os.environ.get("SEPVAD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsepvad.so")
 
 SEPVAD_LN_PLAIN, SEPVAD_LN_RECURSIVE, SEPVAD_LN_RESIDUAL = 0, 1, 2
-SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3 = 0, 1
-PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3}
+SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3, SEPVAD_PREC_F16, SEPVAD_PREC_BF16 = 0, 1, 2, 3
+# fp32 / f16x3: fp32-equivalent (parity path); f16 / bf16: reduced-precision arms (tolerance measured)
+PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVAD_PREC_F16, "bf16": SEPVAD_PREC_BF16}
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
