@@ -424,6 +424,12 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     q[PB_SX] = bo.sx;
     q[PB_SXN] = i + 1 < h->nblk ? h->blk[i + 1].sx : 1.f;
     q[PB_EPS2] = bo.eps2;
+    {
+      double sf = 0.0, sb = 0.0;  // fixed order (bitwise reproducible)
+      for (int k = 0; k < CH; ++k) { sf += pk.blob[bo.fc2 + k]; sb += pk.blob[bo.b2 + k]; }
+      q[PB_SFC2] = (float)sf;
+      q[PB_SB2] = (float)sb;
+    }
     std::memcpy(q + PB_WSUM, bo.wsum, sizeof(bo.wsum));
     const int li = i % h->cfg.layer;
     if (bo.dil != (li == 0 ? 1 : (li % 4 + 1))) { g_err = "fused TCN: dilation schedule mismatch"; return SEPVAD_E_ARG; }
@@ -845,6 +851,8 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.prec = h->prec;
     ta.wfrag = h->prec == PREC_F16X3 ? h->twf : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
     ta.prm = h->tprm;
+    ta.inv_ch = 1.0 / ((double)CH * T);
+    ta.inv_hid = 1.0 / ((double)HID * T);
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
@@ -852,14 +860,15 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     int ngroups = std::min(B, h->tcn_cap_p[h->prec] / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;
-    // epochs per launch and group: 1 (XCD ids) + 4 per block per utterance, < 2^TCN_EPOCH_BITS
+    // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
+    // counted as 4 (headroom)
     // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)
     int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / (4 * h->nblk);
     if (const int mi = env_int("SEPVAD_TCN_MAX_ITER", 0)) max_iter = std::min(max_iter, mi);
     if (max_iter < 1) return fail(SEPVAD_E_ARG, "fused TCN: too many blocks");
     const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
-    const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16;
+    const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16 * 9;  // wave-0 region + per-wave region
     for (int u0 = 0; u0 < B; u0 += per_launch) {
       const int Bl = std::min(per_launch, B - u0);
       const int ng = std::min(ngroups, Bl);
@@ -896,7 +905,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         if (FILE* f = fopen(probe_path, "wb")) {
           const long long hdr[4] = {(long long)ngl * G, h->nblk, G, T};
           fwrite(hdr, sizeof(hdr), 1, f);
-          fwrite(hp.data(), sizeof(unsigned long long), (size_t)ngl * G * h->nblk * 16, f);
+          const size_t n0 = (size_t)ngl * G * h->nblk * 16;
+          fwrite(hp.data(), sizeof(unsigned long long), n0, f);
+          fwrite(hp.data() + n0, sizeof(unsigned long long), n0 * 8, f);  // per-wave stamps (kernel layout)
           fclose(f);
         }
       }

@@ -171,6 +171,29 @@ __device__ __forceinline__ void gn_moments(double s, double ss, double cnt, floa
   rstd = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// The same from a precomputed inv = 1 / cnt, finished in float (torch's CPU GroupNorm computes rstd in
+// float as well): no double division or square root on the persistent kernel's critical path. The sums
+// stay double (E[x^2] - E[x]^2 cancels).
+__device__ __forceinline__ void gn_moments_f(double s, double ss, double inv, float eps, float& mu, float& rstd) {
+  const double m = s * inv;
+  const double var = ss * inv - m * m;
+  mu = (float)m;
+  rstd = 1.f / sqrtf(fmaxf((float)var, 0.f) + eps);
+}
+
+// recursive_moments (below) with gn_moments_f
+__device__ __forceinline__ void recursive_moments_f(const double* m, const double* wsum, float eps_a, float eps_b,
+                                                    double inv, double Tn, float& mua_f, float& rsa, float& mub_f,
+                                                    float& rsb) {
+  gn_moments_f(m[2], m[3], inv, eps_a, mua_f, rsa);
+  const double ra = rsa, mu = mua_f;
+  const double gs = wsum[0], bs = wsum[1], bbs = wsum[2], gbs = wsum[3], ggs = wsum[4];
+  const double sv = m[0] + ra * (m[5] - mu * Tn * gs) + Tn * bs;
+  const double svv = m[1] + 2.0 * m[4] + Tn * bbs + 2.0 * ra * (m[6] - mu * m[7] + m[8] - mu * Tn * gbs) +
+                     ra * ra * (m[9] - 2.0 * mu * m[10] + mu * mu * Tn * ggs);
+  gn_moments_f(sv, svv, inv, eps_b, mub_f, rsb);
+}
+
 // GroupNorm affine from acc = {sum, sumsq}: s[k] = rstd*g[k], h[k] = be[k] - s[k]*mean.
 __device__ __forceinline__ void gn_affine(const double* acc, int K, int T, float eps, const float (&g)[2],
                                           const float (&be)[2], float* s, float* h) {

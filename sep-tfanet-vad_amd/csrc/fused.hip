@@ -44,6 +44,20 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
+// A/B switches (tools/ab_variants.sh builds one library per setting)
+#ifndef TCN_PRIO
+#define TCN_PRIO 0   // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md "Static priority for the younger half")
+#endif
+#ifndef TCN_FMOM
+#define TCN_FMOM 1   // GroupNorm moments finished in float from double sums (no f64 div / sqrt)
+#endif
+#ifndef TCN_MOM5
+#define TCN_MOM5 1   // recursive-LN moment record from 5 per-thread row sums, channel weights applied once
+#endif
+#ifndef TCN_EPI
+#define TCN_EPI 1    // conv1d epilogue parameters from global into registers: no barrier before the epilogue
+#endif
+
 constexpr int NTHR = 512;         // 8 waves; wave w owns output channels [32w, 32w+32) of both GEMMs
 constexpr int LDX = CH + 8;       // x' row stride (halves): 132 dwords == 4 (mod 64) => conflict-free b128 reads
 constexpr int LDD = HID + 8;      // d row stride (halves): 260 dwords == 4 (mod 64)
@@ -266,11 +280,16 @@ __device__ __forceinline__ void gn_affine_ch(int tid, const double* acc, int T, 
 }
 
 // diagnostics (SEPVAD_TCN_PROBE): wave 0's wall clock at 13 phase points of every block of the first
-// utterance each workgroup processes: probe[(blockIdx * nblk + block) * 16 + point]
+// utterance each workgroup processes: probe[(blockIdx * nblk + block) * 16 + point]; and every wave's at the
+// same points (lane 0 of each wave) after that region: probe[grid*nblk*16 + ((blockIdx*nblk + block)*16 + point)*8 + wave]
 #define TPROBE(k)                                                                                  \
   do {                                                                                             \
-    if (a.probe != nullptr && tid == 0 && u == grp)                                                \
-      a.probe[((size_t)blockIdx.x * a.nblk + bi) * 16 + (k)] = wall_clock64();                     \
+    if (a.probe != nullptr && (tid & 63) == 0 && u == grp) {                                       \
+      const unsigned long long _t = wall_clock64();                                                \
+      const size_t _i = ((size_t)blockIdx.x * a.nblk + bi) * 16 + (k);                            \
+      if (tid == 0) a.probe[_i] = _t;                                                              \
+      a.probe[(size_t)gridDim.x * a.nblk * 16 + _i * 8 + (tid >> 6)] = _t;                         \
+    }                                                                                              \
   } while (0)
 
 // DPP lane reductions (no LDS round trip, fixed order => deterministic). update_dpp with old = 0:
@@ -360,6 +379,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const int G = a.G;
+  if (TCN_PRIO && wave_s >= 4) __builtin_amdgcn_s_setprio(1);
   // block -> (group, member): members of a group on one XCD when the grid is a multiple of 8*G
   int grp, g;
   if (gridDim.x % (8 * G) == 0) {
@@ -500,6 +520,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (idx < PB_SIZE / 4) pv[k] = src[idx];
         }
       }
+#if TCN_EPI
+      // the epilogue's per-channel values straight into registers (no LDS round trip, no barrier)
+      const float* pgl = a.prm + (size_t)bi * PB_SIZE;
+      const float ws1 = pgl[PB_WS1 + m], b1 = pgl[PB_B1 + m], a1 = unif(pgl[PB_A1]);
+#endif
       const unsigned e1 = ++ep, tag1 = a.tag0 + e1;
       // ================= conv1d 256->256 (model/model.py:132) + PReLU =================
       f32x16v acc;
@@ -515,8 +540,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int idx = tid + k * NTHR;
           if (idx < PB_SIZE / 4) reinterpret_cast<float4*>(sm.prm)[idx] = pv[k];
         }
+#if TCN_EPI
+        const float ws = ws1, bias = b1;  // block_sums' barrier below makes the blob visible to later phases
+#else
         __syncthreads();
         const float ws = pm[PB_WS1 + m], bias = pm[PB_B1 + m], a1 = pm[PB_A1];
+#endif
         u64* s1 = slot(g, e1);
         float st[2] = {0.f, 0.f};
 #pragma unroll
@@ -578,7 +607,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         {
           const double2 acc = member_sums2(sm.gw, G, lane);
           float mu, rs;
+#if TCN_FMOM
+          gn_moments_f(acc.x, acc.y, a.inv_ch, 1e-8f, mu, rs);
+#else
           gn_moments(acc.x, acc.y, (double)CH * T, 1e-8f, mu, rs);
+#endif
           sc = rs * pm[PB_G1 + c];
           sh = pm[PB_BE1 + c] - sc * mu;
         }
@@ -655,7 +688,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float fmu, frs;
         {
           const double2 acc = member_sums2(sm.gw, G, lane);  // every member's GN2 sums, member order
+#if TCN_FMOM
+          gn_moments_f(acc.x, acc.y, a.inv_hid, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
+#else
           gn_moments(acc.x, acc.y, (double)HID * T, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
+#endif
         }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
         float rsum = 0.f, csr[16];
@@ -752,6 +789,30 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // moment record of u = o + r' (r' = r a_f a_t), see device_common.h recursive_affine
         const float ga = LM == LD_RECURSIVE ? pm[PB_LNAG + m] : 0.f, be = LM == LD_RECURSIVE ? pm[PB_LNAB + m] : 0.f;
         float mo[NMOM];
+#if TCN_MOM5
+        {  // per-thread sums over its 16 rows first, then the channel weights once (same record, fewer VALU)
+          float so = 0.f, soo = 0.f, su = 0.f, suu = 0.f, sou = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int tl = trow(r);
+            const float vm = (t0 + tl < T) ? 1.f : 0.f;  // masked, not branched
+            const float rp = vm * rv[r];
+            if constexpr (LM == LD_RECURSIVE) {
+              const float ov = vm * o[r], uv = ov + rp;
+              so += ov; soo = fmaf(ov, ov, soo); su += uv; suu = fmaf(uv, uv, suu); sou = fmaf(ov, uv, sou);
+            } else {
+              su += rp; suu = fmaf(rp, rp, suu);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NMOM; ++j) mo[j] = 0.f;
+          mo[2] = su; mo[3] = suu;
+          if constexpr (LM == LD_RECURSIVE) {
+            mo[0] = so; mo[1] = soo; mo[4] = be * so; mo[5] = ga * su; mo[6] = ga * sou; mo[7] = ga * so;
+            mo[8] = ga * be * su; mo[9] = ga * ga * suu; mo[10] = ga * ga * su;
+          }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < NMOM; ++j) mo[j] = 0.f;
 #pragma unroll
@@ -767,6 +828,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             mo[2] += rp; mo[3] += rp * rp;
           }
         }
+#endif
         block_sums<NMOM>(mo, sm.red, sm.dred);
       TPROBE(10);
         // ---- P4 words: the moment record (11 doubles); consume every member's ----
@@ -796,13 +858,22 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         for (int j = 0; j < NMOM; ++j) ms[j] = readlane_d(sj, j);
         if constexpr (LM == LD_RECURSIVE) {
           float mua, rsa, mub, rsb;
+#if TCN_FMOM
+          recursive_moments_f(ms, reinterpret_cast<const double*>(pm + PB_WSUM), 1e-5f, 1e-5f, a.inv_ch, (double)T, mua,
+                              rsa, mub, rsb);
+#else
           recursive_moments(ms, reinterpret_cast<const double*>(pm + PB_WSUM), 1e-5f, 1e-5f, CH, T, mua, rsa, mub,
                             rsb);
+#endif
           kc[0] = rsa * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mua;  // as recursive_affine
           kc[2] = rsb * pm[PB_LNBG + m]; kc[3] = pm[PB_LNBB + m] - kc[2] * mub;
         } else {
           float mu, rs;
+#if TCN_FMOM
+          gn_moments_f(ms[2], ms[3], a.inv_ch, 1e-5f, mu, rs);  // as gn_affine
+#else
           gn_moments(ms[2], ms[3], (double)CH * T, 1e-5f, mu, rs);  // as gn_affine
+#endif
           kc[0] = rs * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mu;
         }
       TPROBE(13);

@@ -244,7 +244,8 @@ constexpr int PB_A1 = 4884, PB_A2 = 4885;                          // PReLU slop
 constexpr int PB_SX = 4886, PB_SXN = 4887;                         // fp16 range scale of this / the next block's x'
 constexpr int PB_WSUM = 4888;                                      // 5 doubles (8-byte aligned)
 constexpr int PB_EPS2 = 4898;                                      // reg2 eps, rescaled with d (see api.hip range guard)
-constexpr int PB_SIZE = 4900;                                      // multiple of 4 (float4 staging)
+constexpr int PB_SFC2 = 4899, PB_SB2 = 4900;                       // sum_c fc2[c], sum_c b2[c] (frame means of r)
+constexpr int PB_SIZE = 4904;                                      // multiple of 4 (float4 staging)
 // fp16 hi/lo weights of one block in MFMA fragment order: conv1d hi | lo (256x256) | res_out hi | lo (256x512)
 constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
 // single-plane (PREC_F16 / PREC_BF16) blobs: conv1d (256x256) | res_out (256x512)
@@ -264,6 +265,7 @@ struct TcnArgs {
   unsigned* herr;        // host-mapped (pinned) copy of the same word, read by the host without a sync
   unsigned spin_limit;   // poll passes before a wait gives up (default 1 << 20)
   int force_err;         // diagnostics (SEPVAD_TCN_FORCE_GIVEUP): report a give-up without one happening
+  double inv_ch, inv_hid;  // 1 / (CH * T), 1 / (HID * T): GroupNorm counts
   int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
                          // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)

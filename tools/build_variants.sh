@@ -1,0 +1,19 @@
+# Build A/B variants of libsepvad.so that differ only in fused.hip compile-time switches.
+# usage: bash tools/build_variants.sh name1="-DTCN_X=0" name2="-DTCN_Y=0 -DTCN_Z=0" ...   -> var/lib_<name>.so
+set -e
+cd "$(dirname "$0")/.."
+make -s -C sep-tfanet-vad_amd/csrc ARCH=gfx950
+mkdir -p var
+objs=$(ls sep-tfanet-vad_amd/csrc/build/*.o | grep -v '/fused.o$')
+for spec in "$@"; do
+  name=${spec%%=*}; flags=${spec#*=}
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-variable $flags \
+      -c sep-tfanet-vad_amd/csrc/fused.hip -o var/fused_$name.o &
+done
+wait
+for spec in "$@"; do
+  name=${spec%%=*}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/lib_$name.so var/fused_$name.o $objs
+  rm -f var/fused_$name.o
+done
+ls -la var/

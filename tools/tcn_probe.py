@@ -17,7 +17,7 @@ SUB = [(13, 11, "x': moments->affines"), (14, 13, "x': prefetch issue"), (12, 14
 def main(path):
     raw = np.fromfile(path, dtype=np.int64)
     grid, nblk, G, T = (int(v) for v in raw[:4])
-    full = raw[4:].astype(np.float64).reshape(grid, nblk, 16) / 100.0  # us
+    full = raw[4:4 + grid * nblk * 16].astype(np.float64).reshape(grid, nblk, 16) / 100.0  # us
     st = full[:, :, :13]
     ok = (st > 0).all(axis=2)
     d = np.diff(st, axis=2)  # [grid, nblk, 12]
@@ -46,6 +46,19 @@ def main(path):
     for i, n in enumerate(NAMES):
         v = d[:, 1:, i]  # skip block 0 (cold)
         print(f"  {n:24s} median {np.median(v):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f} us")
+    # per-wave stamps (lane 0 of each wave) after the wave-0 region: arrival spread at every phase point,
+    # per-wave phase durations (which waves a barrier waits for)
+    n0 = grid * nblk * 16
+    if raw.size >= 4 + 9 * n0:
+        W = raw[4 + n0: 4 + 9 * n0].astype(np.float64).reshape(grid, nblk, 16, 8) / 100.0
+        Ws = W[:, 1:, :13, :]
+        if (Ws > 0).all():
+            print("  per-wave: phase                 spread-at-end  per-wave median durations w0..w7 (us)")
+            dw = np.diff(Ws, axis=2)  # [grid, nblk-1, 12, 8]
+            for i, n in enumerate(NAMES):
+                spread = Ws[:, :, i + 1, :].max(axis=2) - Ws[:, :, i + 1, :].min(axis=2)
+                med = np.median(dw[:, :, i, :], axis=(0, 1))
+                print(f"    {n:24s} {np.median(spread):6.2f}   " + " ".join(f"{v:5.2f}" for v in med))
     # optional sub-phase stamps (slots 13..15) splitting one phase: (slot, previous stamp, label)
     for k, prev, label in SUB:
         v = full[:, 1:, k]
