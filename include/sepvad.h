@@ -126,6 +126,14 @@ int32_t sepvad_set_fused(sepvad_handle h, int32_t on);
  * (a bounded wait timed out; outputs of that forward are invalid). */
 int32_t sepvad_fused_status(sepvad_handle h, int32_t* used);
 
+/* The side attributes of the LAST forward on `stream` (self.spectrum, self.masks_b, self.mask_per_speaker,
+ * reference model/model.py:412-429), materialised from that stream's workspace: `out->spectrum`, `out->masks_b`
+ * and `out->mask` (each nullable; the other members are ignored) receive exactly the values the forward would
+ * have written to them. Valid until the next forward on the same stream. The Python host calls this when
+ * one of the attributes is first read, so a forward whose side attributes nobody reads does not pay for
+ * their bin-major copies. SEPVAD_E_ARG if no forward ran on `stream`. */
+int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream);
+
 /* Front-end / back-end stages alone, for kernel-level parity tests:
  * STFT with DC zeroed (model/model.py:16-25,408-410) -> X [B, n_fft/2+1, T] complex64, and
  * 10 log10(clamp(|X|^2, 1e-10)) (model/model.py:411-412) -> spec [B, n_fft/2+1, T] (nullable). */

@@ -105,6 +105,7 @@ struct StreamCtx {
   unsigned* herr_dev = nullptr;         // its device address
   unsigned reported = 0;                // last give-up word already returned to the caller
   unsigned tsalt = 0;                   // launch counter (hand-off tag salt)
+  int last_B = 0, last_N = 0;           // shape of the last forward on this stream (sepvad_side_outputs)
 };
 
 }  // namespace
@@ -1058,6 +1059,8 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   if (rc) return rc;
   rc = ws_reserve(cx, B, N);
   if (rc) return rc;
+  cx->last_B = B;
+  cx->last_N = N;
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   h->ev.clear();
   // diagnostics probe (single chunk only)
@@ -1166,6 +1169,32 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
     if (r && rc == SEPVAD_OK) rc = r;
   }
   return rc;
+}
+
+int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream) {
+  if (!h || !out) return fail(SEPVAD_E_ARG, "sepvad_side_outputs: null argument");
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  StreamCtx* cx = nullptr;
+  for (auto& c : h->ctx)
+    if (c->stream == stream) cx = c.get();
+  if (!cx || cx->last_B < 1) return fail(SEPVAD_E_ARG, "sepvad_side_outputs: no forward has run on this stream");
+  const int B = cx->last_B, N = cx->last_N, T = 1 + N / HOP, Tp = round_up(T, TILE);
+  const hipStream_t s = (hipStream_t)stream;
+  const Workspace w = ws_view(cx->ws, 0, Tp);
+  if (out->spectrum) {  // the gated dB spectrum, recomputed from the dB spectrum (same arithmetic as k_gate)
+    GateArgs ga{};
+    ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = h->cfg.activity_input;
+    ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = nullptr; ga.out_rec = nullptr;
+    ga.spec_side = out->spectrum;
+    HIPCHK(launch_gate(ga, s));
+  }
+  if (out->masks_b || out->mask) {
+    MaskSideArgs m{};
+    m.B = B; m.T = T; m.Tp = Tp; m.masks = w.masks; m.masks_b = out->masks_b; m.mask = out->mask;
+    HIPCHK(launch_mask_side(m, s));
+  }
+  return SEPVAD_OK;
 }
 
 int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {

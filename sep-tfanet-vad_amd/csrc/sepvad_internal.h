@@ -132,9 +132,9 @@ struct GateArgs {
   int B, T, Tp, activity;
   const float* specdb;   // [B][Tp][SPEC_LD]
   const float* w;        // activity_input.weight [9] ; bias at w[9]; prelu at w[10]
-  float* S0;             // [B][Tp][CH] gated bins 1..256
+  float* S0;             // [B][Tp][CH] gated bins 1..256 (nullable: side-output pass)
   float* spec_side;      // nullable [B][NBIN][T] (self.spectrum)
-  double* out_rec;       // [B][Tp/GATE_ROWS][2]
+  double* out_rec;       // [B][Tp/GATE_ROWS][2] (nullable: side-output pass)
 };
 constexpr int GATE_ROWS = 16;
 
@@ -278,6 +278,13 @@ hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);
 hipError_t launch_att_stats(const AttStatsArgs& a, hipStream_t s);
 hipError_t launch_head_stats(const HeadStatsArgs& a, hipStream_t s);
 hipError_t launch_gate(const GateArgs& a, hipStream_t s);
+struct MaskSideArgs {    // bin-major copies of the head output (side attributes, materialised on access)
+  int B, T, Tp;
+  const float* masks;    // [B][Tp][MOUT_PAD] pre-sigmoid
+  float* masks_b;        // nullable [B][MOUT][T]
+  float* mask;           // nullable [B][MOUT][T] sigmoid
+};
+hipError_t launch_mask_side(const MaskSideArgs& a, hipStream_t s);
 hipError_t launch_stft(const StftArgs& a, hipStream_t s);
 hipError_t launch_vad1(const Vad1Args& a, hipStream_t s);
 hipError_t launch_istft(const IstftArgs& a, hipStream_t s);

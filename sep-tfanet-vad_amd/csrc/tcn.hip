@@ -53,11 +53,12 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
       y = x * prelu_f(g, alpha);
     }
     G[ti][f] = y;
-    if (f >= 1) a.S0[((size_t)b * a.Tp + t) * CH + f - 1] = y;
+    if (a.S0 != nullptr && f >= 1) a.S0[((size_t)b * a.Tp + t) * CH + f - 1] = y;
     if (t < T && f >= 1) { st[0] += y; st[1] += y * y; }
   }
   const int nrec = a.Tp / R;
-  block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
+  if (a.out_rec != nullptr) block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
+  else lds_sync();  // G complete (side-output pass: sepvad_side_outputs)
   if (a.spec_side) {  // self.spectrum, [B][257][T]: 16 consecutive frames per bin
     for (int i = tid; i < NBIN * R; i += 256) {
       const int f = i / R, ti = i % R, t = t0 + ti;
@@ -280,6 +281,35 @@ __global__ __launch_bounds__(256) void k_head_stats(HeadStatsArgs a) {
   }
   const int nrec = a.Tp / R;
   block_reduce_store<2>(st, red, a.out_rec + ((size_t)b * nrec + blockIdx.y) * 2);
+}
+
+// ------------------------------------------------------------------------------------------
+// Side attributes of the last forward, materialised on first access (sepvad_side_outputs): the pre-sigmoid
+// masks (self.masks_b, model/model.py:421) and their sigmoid (self.mask_per_speaker, :429), bin-major, from
+// the frame-major head output still in the workspace. 16 frames per workgroup through an LDS transpose.
+constexpr int SIDE_FR = 16;
+__global__ __launch_bounds__(256) void k_mask_side(MaskSideArgs a) {
+  __shared__ float tile[SIDE_FR][MOUT + 1];
+  const int b = blockIdx.x, t0 = blockIdx.y * SIDE_FR, tid = threadIdx.x;
+  const int nf = min(SIDE_FR, a.T - t0);
+  for (int i = tid; i < SIDE_FR * MOUT; i += 256) {
+    const int fi = i / MOUT, c = i - fi * MOUT;
+    if (fi < nf) tile[fi][c] = a.masks[((size_t)b * a.Tp + t0 + fi) * MOUT_PAD + c];
+  }
+  lds_sync();
+  for (int i = tid; i < MOUT * SIDE_FR; i += 256) {
+    const int c = i / SIDE_FR, fi = i - c * SIDE_FR;
+    if (fi >= nf) continue;
+    const float v = tile[fi][c];
+    const size_t o = ((size_t)b * MOUT + c) * a.T + t0 + fi;  // [B][514][T] == [B][2][257][T]
+    if (a.masks_b) a.masks_b[o] = v;
+    if (a.mask) a.mask[o] = sigmoid_f(v);
+  }
+}
+
+hipError_t launch_mask_side(const MaskSideArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_mask_side, dim3(a.B, (a.T + SIDE_FR - 1) / SIDE_FR), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_head_stats(const HeadStatsArgs& a, hipStream_t s) {

@@ -10,7 +10,11 @@ reference checkpoint. ``forward`` keeps the reference contract:
   ``inference_kw['return_smoothed_vad']``, or the int 0 when ``final_vad`` is False
   (model/model.py:424-427,456-457,461);
 * sets ``self.spectrum``, ``self.masks_b``, ``self.mask_per_speaker`` (post-sigmoid) and
-  ``self.estimated_stfts`` (model/model.py:412,421,429,437-439).
+  ``self.estimated_stfts`` (model/model.py:412,421,429,437-439). In the reference the first three are
+  views of intermediates (free); here they are bin-major copies of frame-major device buffers, so they are
+  materialised on first read (``sepvad_side_outputs``, same values) from the workspace of the forward that
+  produced them — a forward whose side attributes nobody reads does not write them. Assigning to them
+  works as for plain attributes.
 
 All arithmetic runs in ``libsepvad.so`` through the C ABI of ``include/sepvad.h``; there is no
 CPU fallback — a CPU tensor or a missing library raises.
@@ -185,6 +189,29 @@ class SeparationModel(nn.Module):
             h.set_precision(self.native_precision)
         return h
 
+    # -- side attributes (model/model.py:412,421,429), materialised on first read ---------------------
+    _SIDE_NAMES = ("spectrum", "masks_b", "mask_per_speaker")
+
+    def _side_get(self, name):
+        cache = self.__dict__.setdefault("_side_cache", {})
+        if name not in cache:
+            src = self.__dict__.get("_side_src")
+            if src is None:
+                raise AttributeError(f"'SeparationModel' has no attribute '{name}' before the first forward")
+            h, stream, B, T = src
+            # masks_b and mask_per_speaker come from one kernel: materialise both together
+            want = (name,) if name == "spectrum" else tuple(n for n in ("masks_b", "mask_per_speaker") if n not in cache)
+            cache.update(h.side_outputs(stream, B, T, want))
+        return cache[name]
+
+    def _side_set(self, name, value):
+        self.__dict__.setdefault("_side_cache", {})[name] = value
+
+    spectrum = property(lambda self: self._side_get("spectrum"), lambda self, v: self._side_set("spectrum", v))
+    masks_b = property(lambda self: self._side_get("masks_b"), lambda self, v: self._side_set("masks_b", v))
+    mask_per_speaker = property(lambda self: self._side_get("mask_per_speaker"),
+                                lambda self, v: self._side_set("mask_per_speaker", v))
+
     # -- forward (model/model.py:402-461) --------------------------------------------------------
     def forward(self, x: torch.Tensor, inference_kw: dict = {}):  # noqa: B006  (reference signature)
         assert x.ndim == 2, "input tensor must be 2 dimensions (B, T), but got dimensions of {}".format(x.ndim)
@@ -192,9 +219,8 @@ class SeparationModel(nn.Module):
             raise RuntimeError("SeparationModel (MI355X build) runs on a ROCm device only: "
                                "move the model and the input to 'cuda' (there is no CPU path)")
         h = self.native_handle(x.device)
-        out = h.forward(x, inference_kw if inference_kw else None, return_aux=True)
-        self.spectrum = out["spectrum"]
-        self.masks_b = out["masks_b"]
-        self.mask_per_speaker = out["mask_per_speaker"]
+        out = h.forward(x, inference_kw if inference_kw else None)
+        self.__dict__["_side_src"] = (h, out["stream"], out["B"], out["T"])
+        self.__dict__["_side_cache"] = {}
         self.estimated_stfts = out["est"]
         return out["sep"], out["vad"], out["est"]

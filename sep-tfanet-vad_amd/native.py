@@ -22,7 +22,8 @@ PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVA
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
-    "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_stft", "sepvad_istft", "sepvad_pit_l1", "sepvad_stream_append",
+    "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_stft", "sepvad_istft",
+    "sepvad_pit_l1", "sepvad_stream_append",
     "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_rir_generate",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
@@ -82,6 +83,8 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_set_fused.argtypes = [P, i32]
     lib.sepvad_fused_status.restype = i32
     lib.sepvad_fused_status.argtypes = [P, ctypes.POINTER(i32)]
+    lib.sepvad_side_outputs.restype = i32
+    lib.sepvad_side_outputs.argtypes = [P, ctypes.POINTER(SepVadOutputs), P]
     lib.sepvad_stft.restype = i32
     lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft.restype = i32
@@ -253,8 +256,9 @@ class Handle:
         outs = SepVadOutputs(_ptr(sep).value, _ptr(vad).value, _ptr(est).value, _ptr(spectrum).value,
                              _ptr(masks_b).value, _ptr(mask).value)
         kw = make_kw(inference_kw)
+        stream = self._stream()
         rc = self._lib.sepvad_forward_strided(self._h, _ptr(x), ldx, B, N, ctypes.byref(outs),
-                                              ctypes.byref(kw) if kw is not None else None, self._stream())
+                                              ctypes.byref(kw) if kw is not None else None, stream)
         _check(rc, "sepvad_forward")
         if CHECK_EACH_FORWARD:
             self.fused_status()  # synchronises; raises if this forward's fused TCN gave up
@@ -264,9 +268,33 @@ class Handle:
             vad_ret = vad.view(B, S, 1, T)  # model/model.py:456-457
         else:
             vad_ret = vad
-        res = dict(sep=sep, vad=vad_ret, est=est)
+        res = dict(sep=sep, vad=vad_ret, est=est, stream=stream.value or 0, B=B, T=T)
         if return_aux:
             res.update(spectrum=spectrum, masks_b=masks_b, mask_per_speaker=mask)
+        return res
+
+    def side_outputs(self, stream: int, B: int, T: int, want=("spectrum", "masks_b", "mask_per_speaker")):
+        """The side attributes of the last forward on `stream` (sepvad_side_outputs), materialised now on that
+        stream: dict with the requested subset of spectrum [B,257,T], masks_b [B,514,T] and
+        mask_per_speaker [B,2,257,T]."""
+        F = self.cfg["n_fftBins"] // 2 + 1
+        S = self.cfg["num_spk"]
+        cur = torch.cuda.current_stream(self.device)
+        ctx = torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)) if cur.cuda_stream != stream \
+            else torch.cuda.stream(cur)
+        res = {}
+        with ctx:
+            dev = self.device
+            if "spectrum" in want:
+                res["spectrum"] = torch.empty(B, F, T, device=dev, dtype=torch.float32)
+            if "masks_b" in want:
+                res["masks_b"] = torch.empty(B, S * F, T, device=dev, dtype=torch.float32)
+            if "mask_per_speaker" in want:
+                res["mask_per_speaker"] = torch.empty(B, S, F, T, device=dev, dtype=torch.float32)
+            outs = SepVadOutputs(0, 0, 0, _ptr(res.get("spectrum")).value, _ptr(res.get("masks_b")).value,
+                                 _ptr(res.get("mask_per_speaker")).value)
+            _check(self._lib.sepvad_side_outputs(self._h, ctypes.byref(outs), ctypes.c_void_p(stream)),
+                   "sepvad_side_outputs")
         return res
 
     def stft(self, x: torch.Tensor):
