@@ -134,6 +134,13 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used);
  * their bin-major copies. SEPVAD_E_ARG if no forward ran on `stream`. */
 int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream);
 
+/* Block-level parity probe of the fused TCN: while `dump` (device, >= 3 * B * roundup(T, 64) * 256 floats) is
+ * set, forwards that run the fused TCN in one launch write dump[0] = TCN.LN output x'_0 (model/model.py:333),
+ * dump[1] = block 0's DepthConv1d output (:144) and dump[2] = block 0's TF_Attention output (:207), each
+ * [B][roundup(T, 64)][256] channel-last. NULL disables. F16X3 arithmetic only (a separate instantiation of the
+ * kernel); tests only (the reference golden's tcn_in, blk0_res, blk0_att). */
+int32_t sepvad_set_tcn_dump(sepvad_handle h, float* dump);
+
 /* Front-end / back-end stages alone, for kernel-level parity tests:
  * STFT with DC zeroed (model/model.py:16-25,408-410) -> X [B, n_fft/2+1, T] complex64, and
  * 10 log10(clamp(|X|^2, 1e-10)) (model/model.py:411-412) -> spec [B, n_fft/2+1, T] (nullable). */
@@ -168,6 +175,13 @@ int32_t sepvad_stream_append(const float* src, int64_t src_ld, int64_t s0, int32
  * double, fixed-order reductions (bitwise reproducible). Device pointers, stream-ordered. */
 int32_t sepvad_si_sdr(const float* P, int64_t p_ld, const float* Tg, int64_t t_ld, int64_t N, int32_t R,
                       const int32_t* pidx, const int32_t* tidx, int32_t zero_mean, float* out, void* stream);
+
+/* Replaces Accuracy_Vad()(preds, targets, _) (model/metric.py:163-177): labels = preds > 0.5 (NaN kept),
+ * written back into preds when in_place (the reference masks its argument in place); out[0] = fraction of
+ * labels equal to targets over [B, S, T], out[1 + s] = the same for speaker s (S <= 8). Device pointers,
+ * contiguous [B][S][T] f32, stream-ordered; integer counts (exact). */
+int32_t sepvad_vad_accuracy(float* preds, const float* targets, int32_t B, int32_t S, int32_t T, int32_t in_place,
+                            float* out, void* stream);
 
 /* ---- synthetic reverberant mixtures (BASELINE cfg 4): image-method room impulse responses --------
  * Replaces pyrirgen.generateRir / gen_rir (create_data/rirgen.cpp:115-351, create_data/pyrirgen.pyx)

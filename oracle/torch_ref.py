@@ -233,3 +233,18 @@ def si_sdr(preds, target, zero_mean=True):
     ts = alpha * target
     noise = ts - preds
     return 10 * torch.log10(((ts ** 2).sum(-1) + eps) / ((noise ** 2).sum(-1) + eps))
+
+
+def accuracy_vad(preds, targets):
+    """Accuracy_Vad (reference model/metric.py:163-177) on numpy arrays [B, S, T]: labels = preds > 0.5
+    (in the reference's order: > 0.5 -> 1, then <= 0.5 -> 0, NaN untouched); returns (labels, [acc, acc0, acc1])
+    in float32 like torch's int64-sum / numel."""
+    import numpy as np
+    p = np.array(preds, dtype=np.float32, copy=True)
+    p[p > 0.5] = 1
+    p[p <= 0.5] = 0
+    eq = p == targets
+    n = np.float32(targets.size)
+    accs = [np.float32(eq.sum()) / n] + [np.float32(eq[:, s].sum()) / np.float32(targets[:, s].size)
+                                         for s in range(targets.shape[1])]
+    return p, np.array(accs, dtype=np.float32)

@@ -142,6 +142,7 @@ struct sepvad_model {
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
+  float* tdump = nullptr;       // parity probe buffer of the fused TCN (sepvad_set_tcn_dump), caller-owned
   // caller-stream contexts (workspace, hand-off words, give-up words); `mu` serialises the host-side
   // enqueue of concurrent callers (the kernels of different streams still overlap on the device)
   std::vector<std::unique_ptr<StreamCtx>> ctx;
@@ -887,6 +888,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       ta.Xfin = w.O[0] + (size_t)u0 * Tp * CH;
       ta.rec_head = w.rec_hs + (size_t)u0 * G * 2;
       ta.probe = nullptr;
+      ta.dump = (h->tdump && u0 == 0 && Bl == B) ? h->tdump : nullptr;
       if (probe_path && u0 == 0) {
         if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
@@ -1157,6 +1159,13 @@ int32_t sepvad_set_fused(sepvad_handle h, int32_t on) {
   return SEPVAD_OK;
 }
 
+int32_t sepvad_set_tcn_dump(sepvad_handle h, float* dump) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->tdump = dump;
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
   DeviceGuard dg(h->device);
@@ -1295,6 +1304,16 @@ int32_t sepvad_si_sdr(const float* P, int64_t p_ld, const float* Tg, int64_t t_l
   a.P = P; a.p_ld = p_ld; a.Tg = Tg; a.t_ld = t_ld; a.N = N; a.R = R; a.pidx = pidx; a.tidx = tidx;
   a.zero_mean = zero_mean; a.out = out;
   HIPCHK(launch_si_sdr(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_vad_accuracy(float* preds, const float* targets, int32_t B, int32_t S, int32_t T, int32_t in_place,
+                            float* out, void* stream) {
+  if (!preds || !targets || !out || B < 1 || S < 1 || S > VACC_MAX_S || T < 1)
+    return fail(SEPVAD_E_ARG, "sepvad_vad_accuracy: bad arguments");
+  VadAccArgs a{};
+  a.preds = preds; a.targets = targets; a.B = B; a.S = S; a.T = T; a.in_place = in_place; a.out = out;
+  HIPCHK(launch_vad_acc(a, (hipStream_t)stream));
   return SEPVAD_OK;
 }
 

@@ -372,7 +372,7 @@ __device__ __forceinline__ KArgs kargs() {
   return p;
 }
 
-template <int LM, int PRE>
+template <int LM, int PRE, bool DUMP = false>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   using WL = WLay<PRE>;
   __shared__ __attribute__((aligned(16))) TcnSmem sm;
@@ -489,6 +489,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const int tl = trow(r);
         o[r] = fmaf(raw[r], s, h) * (t0 + tl < T ? 1.f : 0.f);
         split_store<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
+      }
+      if (float* dp = DUMP ? kargs()->dump : nullptr) {  // parity probe: TCN.LN output (model/model.py:333); pointer re-read
+#pragma unroll                           // from the kernarg segment at use (no register held across the loop)
+        for (int r = 0; r < 16; ++r) dp[((size_t)u * Tp + t0 + trow(r)) * CH + m] = o[r];
       }
     }
     __syncthreads();
@@ -780,9 +784,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // ---- residual update (model/model.py:345-352) ----
       // gate r in place once: r' = r a_f a_t (a_f = a_t = 1 without TF-attention, set at kernel start)
       {
+        if (bi == 0) {  // parity probe: DepthConv1d output of block 0 (model/model.py:144), before the gates
+          if (float* dp = DUMP ? kargs()->dump : nullptr) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dp[((size_t)(kargs()->B + u) * Tp + t0 + trow(r)) * CH + m] = rv[r];
+          }
+        }
         const float afm = sm.af[m];
 #pragma unroll
         for (int r = 0; r < 16; ++r) rv[r] = rv[r] * (afm * sm.at[trow(r)]);
+        if (bi == 0) {  // parity probe: TF_Attention output of block 0 (model/model.py:207)
+          if (float* dp = DUMP ? kargs()->dump : nullptr) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dp[((size_t)(2 * kargs()->B + u) * Tp + t0 + trow(r)) * CH + m] = rv[r];
+          }
+        }
       }
       float kc[4] = {0.f, 0.f, 0.f, 0.f};  // this channel's residual-LN affines (GN_a: 0, 1; GN_b: 2, 3)
       if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
@@ -922,6 +938,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 
 template <int PRE>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
+  if constexpr (PRE == PREC_F16X3) {
+    if (a.dump != nullptr) {  // parity-probe instantiation (the probe code stays out of the production kernels)
+      switch (a.ln_mode) {
+        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
   switch (a.ln_mode) {
     case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
     case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;

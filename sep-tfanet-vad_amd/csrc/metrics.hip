@@ -74,6 +74,51 @@ __global__ __launch_bounds__(SD_THREADS) void k_si_sdr(SiSdrArgs a) {
   }
 }
 
+// VAD accuracy (reference model/metric.py:163-177 Accuracy_Vad): labels = preds > 0.5 (not >=; NaN kept),
+// written back into preds as the reference's in-place masking does (when in_place), then the fraction of
+// labels equal to the targets over everything and per speaker. One workgroup: integer counts, exact.
+__global__ __launch_bounds__(1024) void k_vad_acc(VadAccArgs a) {
+  __shared__ unsigned cnt[1024 / 64][VACC_MAX_S];
+  unsigned c[VACC_MAX_S];
+#pragma unroll
+  for (int s = 0; s < VACC_MAX_S; ++s) c[s] = 0;
+  const long long n = (long long)a.B * a.S * a.T;
+  for (long long i = threadIdx.x; i < n; i += 1024) {
+    const int s = (int)((i / a.T) % a.S);
+    float p = a.preds[i];
+    p = p > 0.5f ? 1.f : (p <= 0.5f ? 0.f : p);
+    if (a.in_place) a.preds[i] = p;
+    const unsigned hit = p == a.targets[i] ? 1u : 0u;
+#pragma unroll
+    for (int q = 0; q < VACC_MAX_S; ++q) c[q] += q == s ? hit : 0u;
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < VACC_MAX_S; ++q) {
+    unsigned v = c[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (l == 0) cnt[w][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int q = 0; q < a.S; ++q) {
+      unsigned long long cq = 0;
+      for (int ww = 0; ww < 1024 / 64; ++ww) cq += cnt[ww][q];
+      tot += cq;
+      a.out[1 + q] = (float)cq / (float)((long long)a.B * a.T);  // torch: int64 sum / int -> float32
+    }
+    a.out[0] = (float)tot / (float)n;
+  }
+}
+
+hipError_t launch_vad_acc(const VadAccArgs& a, hipStream_t s) {
+  if (a.B < 1 || a.S < 1 || a.S > VACC_MAX_S || a.T < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_vad_acc, dim3(1), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_si_sdr(const SiSdrArgs& a, hipStream_t s) {
   if (a.R < 1 || a.N < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_si_sdr, dim3(a.R), dim3(SD_THREADS), 0, s, a);

@@ -227,6 +227,13 @@ struct SiSdrArgs {
   float* out;
 };
 hipError_t launch_si_sdr(const SiSdrArgs& a, hipStream_t s);
+constexpr int VACC_MAX_S = 8;
+struct VadAccArgs {
+  float* preds; const float* targets;   // [B][S][T]
+  int B, S, T, in_place;
+  float* out;                           // [1 + S]: overall, per speaker
+};
+hipError_t launch_vad_acc(const VadAccArgs& a, hipStream_t s);
 hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
 // ---- fused persistent TCN (fused.hip) ----
@@ -269,6 +276,8 @@ struct TcnArgs {
   int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
                          // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
+  float* dump;           // parity probe (sepvad_set_tcn_dump), nullable: [3][B][Tp][CH] = TCN.LN output x'_0,
+                         // block 0's res_out output r and its TF-attention output r * a_f * a_t
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
 int tcn_blocks_per_cu(int ln_mode, int prec);

@@ -10,6 +10,8 @@
   the batch) is restated; parity of that reduction is pinned by the oracle tests, not by torchmetrics.
 * ``SI_SDRi`` / ``si_sdri`` (``model/metric.py:145-160``): ``pit_si_sdr(preds, target)`` minus the mean
   SI-SDR of the mixture against each target.
+* ``Accuracy_Vad`` (``model/metric.py:163-177``): thresholded (``> 0.5``) VAD label accuracy, overall and per
+  speaker; like the reference it thresholds ``preds`` in place (``k_vad_acc``, exact integer counts).
 
 All inputs are ROCm tensors; the arithmetic runs in ``k_si_sdr`` (csrc/metrics.hip) through the C ABI
 ``sepvad_si_sdr``. There is no CPU fallback.
@@ -103,3 +105,24 @@ class SI_SDRi(torch.nn.Module):
 
 si_sdri = SI_SDRi()
 si_sdri.__name__ = "si_sdri"
+
+
+class Accuracy_Vad(torch.nn.Module):
+    """model/metric.py:163-177: preds, targets [B, num_spk, T] -> (acc, acc0, acc1) 0-dim float32 tensors.
+    preds is thresholded in place (> 0.5 -> 1, <= 0.5 -> 0), as the reference does."""
+
+    def forward(self, preds, targets, batch_indices_vad=None):
+        _check_same_shape(preds, targets)
+        if preds.device.type != "cuda" or targets.device != preds.device:
+            raise RuntimeError("sepvad metrics: inputs must be ROCm device tensors on one device")
+        B, S, T = preds.shape
+        work = preds if (preds.dtype == torch.float32 and preds.is_contiguous()) else preds.float().contiguous()
+        tg = targets.to(torch.float32).contiguous()
+        out = torch.empty(1 + S, device=preds.device, dtype=torch.float32)
+        lib = _native.load_library()
+        rc = lib.sepvad_vad_accuracy(_native._ptr(work), _native._ptr(tg), B, S, T, 1, _native._ptr(out),
+                                     torch.cuda.current_stream(preds.device).cuda_stream)
+        _native._check(rc, "sepvad_vad_accuracy")
+        if work is not preds:
+            preds.copy_(work)
+        return out[0], out[1], out[2]

@@ -22,9 +22,11 @@ PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVA
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
-    "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_stft", "sepvad_istft",
+    "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
+    "sepvad_stft", "sepvad_istft",
     "sepvad_pit_l1", "sepvad_stream_append",
-    "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_rir_generate",
+    "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_vad_accuracy",
+    "sepvad_rir_generate",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
 )
 
@@ -83,6 +85,8 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_set_fused.argtypes = [P, i32]
     lib.sepvad_fused_status.restype = i32
     lib.sepvad_fused_status.argtypes = [P, ctypes.POINTER(i32)]
+    lib.sepvad_set_tcn_dump.restype = i32
+    lib.sepvad_set_tcn_dump.argtypes = [P, P]
     lib.sepvad_side_outputs.restype = i32
     lib.sepvad_side_outputs.argtypes = [P, ctypes.POINTER(SepVadOutputs), P]
     lib.sepvad_stft.restype = i32
@@ -102,6 +106,8 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_normalize.argtypes = [P, i64, P, P, P]
     lib.sepvad_si_sdr.restype = i32
     lib.sepvad_si_sdr.argtypes = [P, i64, P, i64, i64, i32, P, P, i32, P, P]
+    lib.sepvad_vad_accuracy.restype = i32
+    lib.sepvad_vad_accuracy.argtypes = [P, P, i32, i32, i32, i32, P, P]
     dptr = ctypes.POINTER(ctypes.c_double)
     lib.sepvad_rir_generate.restype = i32
     lib.sepvad_rir_generate.argtypes = [ctypes.c_double, ctypes.c_double, dptr, i32, dptr, dptr, dptr, i32, dptr,
@@ -296,6 +302,23 @@ class Handle:
             _check(self._lib.sepvad_side_outputs(self._h, ctypes.byref(outs), ctypes.c_void_p(stream)),
                    "sepvad_side_outputs")
         return res
+
+    def tcn_dump(self, x: torch.Tensor):
+        """Block-level parity probe (sepvad_set_tcn_dump): one forward of x with the fused TCN, returning
+        (tcn_in, blk0_res, blk0_att) as [B, 256, T] like the reference module outputs."""
+        B, N = x.shape
+        T = 1 + N // 256
+        Tp = (T + 63) // 64 * 64
+        buf = torch.zeros(3, B, Tp, 256, device=self.device, dtype=torch.float32)
+        _check(self._lib.sepvad_set_tcn_dump(self._h, _ptr(buf)), "sepvad_set_tcn_dump")
+        try:
+            self.forward(x)
+            if not self.fused_status():
+                raise RuntimeError("tcn_dump: the fused TCN did not run")
+        finally:
+            _check(self._lib.sepvad_set_tcn_dump(self._h, None), "sepvad_set_tcn_dump")
+        v = buf[:, :, :T, :].permute(0, 1, 3, 2)
+        return v[0], v[1], v[2]
 
     def stft(self, x: torch.Tensor):
         """STFT with DC zeroed and its dB spectrum (kernel-level test entry)."""

@@ -83,3 +83,24 @@ def test_metrics_reject_host_tensors():
     from sep_tfanet_vad_amd import metrics
     with pytest.raises(RuntimeError):
         metrics.calc_sisdr(torch.zeros(3, 100), torch.zeros(3, 100))
+
+
+def test_metrics_match_reference_goldens():
+    """Device calc_sisdr (both zero_mean branches) and Accuracy_Vad vs outputs of the reference itself
+    (tests/golden/golden_metrics.npz, make_metric_golden.py). Accuracy_Vad thresholds preds in place
+    like the reference (p > 0.5: exactly 0.5 is a 0)."""
+    import os
+    from conftest import GOLDEN
+    from sep_tfanet_vad_amd import metrics
+    g = np.load(os.path.join(GOLDEN, "golden_metrics.npz"))
+    p, t = torch.from_numpy(g["sisdr_preds"]).to("cuda"), torch.from_numpy(g["sisdr_target"]).to("cuda")
+    for zm in (0, 1):
+        v = metrics.calc_sisdr(p, t, zero_mean=bool(zm)).cpu().numpy()
+        assert np.abs(v - g[f"sisdr_zm{zm}"]).max() <= 1e-4  # fp32 reference vs moments in double
+        e = metrics.calc_sisdr(torch.from_numpy(g["ex_preds"]).to("cuda"), torch.from_numpy(g["ex_target"]).to("cuda"),
+                               zero_mean=bool(zm)).item()
+        assert abs(e - float(g[f"ex_zm{zm}"])) <= 1e-5
+    vp = torch.from_numpy(g["vad_preds"]).to("cuda")
+    acc, acc0, acc1 = metrics.Accuracy_Vad()(vp, torch.from_numpy(g["vad_targets"]).to("cuda"), None)
+    assert np.array_equal(vp.cpu().numpy(), g["vad_preds_after"])
+    assert np.array_equal(np.array([acc.item(), acc0.item(), acc1.item()], np.float32), g["vad_acc"])

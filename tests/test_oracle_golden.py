@@ -130,3 +130,21 @@ def test_oracle_si_sdr_known_answer():
     from oracle.torch_ref import si_sdr
     v = si_sdr(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]), zero_mean=False).item()
     assert abs(v - 18.4030) < 1e-4
+
+
+def test_oracle_metrics_match_reference_goldens():
+    """calc_sisdr (model/combined_loss.py:16-56) for zero_mean True (the default) and False, and
+    Accuracy_Vad (model/metric.py:163-177), against outputs of the reference itself
+    (tests/golden/make_metric_golden.py)."""
+    import os
+    from conftest import GOLDEN
+    from oracle.torch_ref import accuracy_vad, si_sdr
+    g = np.load(os.path.join(GOLDEN, "golden_metrics.npz"))
+    for zm in (0, 1):
+        v = si_sdr(torch.from_numpy(g["sisdr_preds"]), torch.from_numpy(g["sisdr_target"]), zero_mean=bool(zm)).numpy()
+        assert np.abs(v - g[f"sisdr_zm{zm}"]).max() <= 1e-4
+        e = si_sdr(torch.from_numpy(g["ex_preds"]), torch.from_numpy(g["ex_target"]), zero_mean=bool(zm)).item()
+        assert abs(e - float(g[f"ex_zm{zm}"])) <= 1e-5
+    labels, acc = accuracy_vad(g["vad_preds"], g["vad_targets"])
+    assert np.array_equal(labels, g["vad_preds_after"])
+    assert np.array_equal(acc, g["vad_acc"])
