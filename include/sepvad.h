@@ -112,6 +112,14 @@ int32_t sepvad_forward(sepvad_handle h, const float* x, int32_t B, int32_t N,
 int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int32_t B, int32_t N,
                                const SepVadOutputs* out, const SepVadInferKw* kw, void* stream);
 
+/* Replaces the window loop of OnlineSaving.calc_online (model/online_class_unknown_targets.py:80-97) as ONE
+ * forward: n_win windows of N samples for each of n_streams signals, window k of stream b starting at
+ * x + b * ld_stream + k * hop (no gather copy); utterance u = k * n_streams + b of the outputs (so window k of
+ * every stream is a contiguous [n_streams, ...] block). Requires (n_win - 1) * hop + N <= ld_stream. */
+int32_t sepvad_forward_windows(sepvad_handle h, const float* x, int64_t ld_stream, int32_t n_streams, int32_t n_win,
+                               int64_t hop, int32_t N, const SepVadOutputs* out, const SepVadInferKw* kw,
+                               void* stream);
+
 /* Split each forward's batch into n (1..4) utterance chunks that run concurrently on internal
  * streams forked from / joined to the caller's stream (results are bitwise identical for any n:
  * every reduction is per utterance). Default 1, or the SEPVAD_SPLIT environment variable. */
@@ -158,9 +166,18 @@ int32_t sepvad_istft(sepvad_handle h, const void* est, int32_t BS, int32_t N, fl
  * the whole batch), loss set over the 2 permutations, first minimum. Writes perm_out [B, 2] int64
  * (batch_indices), loss_out (min loss) and pw_out [2, 2] (pairwise losses), each nullable.
  * scratch: device buffer of at least SEPVAD_PIT_SCRATCH_BYTES. Deterministic. */
-#define SEPVAD_PIT_SCRATCH_BYTES 16384
+#define SEPVAD_PIT_SCRATCH_BYTES 16448
 int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_t ref_ld, int32_t B, int64_t L,
                       void* scratch, int64_t* perm_out, float* loss_out, float* pw_out, void* stream);
+/* The same in two steps, for a stream batch sharded over ranks (nn.L1Loss means over the WHOLE batch,
+ * model/pit_wrapper.py:172-177): sepvad_pit_l1_sums writes this device's 4 pairwise L1 sums (double,
+ * fixed order) to sums[4] (device); the caller all-reduces them over the ranks (RCCL, 32 bytes); then
+ * sepvad_pit_l1_choose turns sums / count (count = total rows x L over all ranks) into the permutation
+ * for this device's B rows, the loss and the pairwise means, exactly as sepvad_pit_l1 does. */
+int32_t sepvad_pit_l1_sums(const float* est, int64_t est_ld, const float* ref, int64_t ref_ld, int32_t B, int64_t L,
+                           void* scratch, double* sums, void* stream);
+int32_t sepvad_pit_l1_choose(const double* sums, double count, int32_t B, int64_t* perm_out, float* loss_out,
+                             float* pw_out, void* stream);
 
 /* Replaces reorder_source_mse(preds, batch_indices) (model/combined_loss.py:63-78) fused with
  * OnlineSaving.update_online_signal (online_class_unknown_targets.py:28-37):

@@ -803,8 +803,16 @@ struct TimingRec {
 };
 
 // Enqueues the forward of utterances [b0, b0 + B) on stream s (model/model.py:402-461).
+// Input row mapping of one forward: utterance u reads x + (u % nstr) * ldx + (u / nstr) * hopw (nstr = 0:
+// plain batch, every row at u * ldx).
+struct XMap {
+  int nstr = 0;
+  long long hopw = 0;
+};
+
 int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b0, int B, int N,
-                  const SepVadOutputs* out, const SepVadInferKw* kw, hipStream_t s, TimingRec* tr) {
+                  const SepVadOutputs* out, const SepVadInferKw* kw, hipStream_t s, TimingRec* tr,
+                  const XMap& xm) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
   const SepVadConfig& c = h->cfg;
@@ -820,6 +828,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   {
     StftArgs sa{};
     sa.B = B; sa.N = N; sa.ldx = ldx; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
+    sa.nstr = xm.nstr > 0 ? xm.nstr : B; sa.hopw = xm.nstr > 0 ? xm.hopw : 0;
     sa.window = h->P(h->win_out);
     sa.X = w.X;
     sa.specdb = h->same_stft_window ? w.specdb : nullptr;
@@ -1051,7 +1060,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
 }
 
 int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const SepVadOutputs* out,
-                 const SepVadInferKw* kw, hipStream_t s) {
+                 const SepVadInferKw* kw, hipStream_t s, const XMap& xm = XMap()) {
   const int T = 1 + N / HOP;
   const int Tp = round_up(T, TILE);
   StreamCtx* cx = nullptr;
@@ -1079,11 +1088,12 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
     HIPCHK(hipMemsetAsync(h->probe, 0, need * sizeof(unsigned long long), s));
     h->probe_blk = atoi(pb);
   }
-  const int nsplit = (h->probe_blk >= 0 || h->timing || fused_ok(h, T)) ? 1 : std::max(1, std::min(h->split, B));
+  const int nsplit = (h->probe_blk >= 0 || h->timing || fused_ok(h, T) || xm.nstr > 0) ? 1
+                                                                                       : std::max(1, std::min(h->split, B));
   TimingRec tr;
   if (nsplit == 1) {
     if (ev_record(h, s)) return SEPVAD_E_HIP;
-    rc = enqueue_chunk(h, cx, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr);
+    rc = enqueue_chunk(h, cx, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr, xm);
     if (rc) return rc;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
   } else {
@@ -1093,7 +1103,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
     for (int k = 0; k < nsplit; ++k) {
       const int bc = B / nsplit + (k < B % nsplit ? 1 : 0);
       HIPCHK(hipStreamWaitEvent(h->sub[k], h->fork, 0));
-      rc = enqueue_chunk(h, cx, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr);
+      rc = enqueue_chunk(h, cx, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr, xm);
       if (rc) return rc;
       HIPCHK(hipEventRecord(h->join[k], h->sub[k]));
       HIPCHK(hipStreamWaitEvent(s, h->join[k], 0));
@@ -1146,6 +1156,23 @@ int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int
   DeviceGuard dg(h->device);
   std::lock_guard<std::mutex> lk(h->mu);
   return forward_impl(h, x, (int)ldx, B, N, out, kw, (hipStream_t)stream);
+}
+
+int32_t sepvad_forward_windows(sepvad_handle h, const float* x, int64_t ld_stream, int32_t n_streams, int32_t n_win,
+                               int64_t hop, int32_t N, const SepVadOutputs* out, const SepVadInferKw* kw,
+                               void* stream) {
+  if (!h || !x || !out || !out->sep) return fail(SEPVAD_E_ARG, "sepvad_forward_windows: null argument");
+  if (n_streams < 1 || n_win < 1 || hop < 0 || (long long)n_streams * n_win > INT32_MAX)
+    return fail(SEPVAD_E_SHAPE, "sepvad_forward_windows: bad window counts");
+  if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward_windows: N must exceed 256");
+  if ((long long)(n_win - 1) * hop + N > ld_stream || ld_stream > INT32_MAX)
+    return fail(SEPVAD_E_SHAPE, "sepvad_forward_windows: windows exceed the stream rows");
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  XMap xm;
+  xm.nstr = n_streams;
+  xm.hopw = hop;
+  return forward_impl(h, x, (int)ld_stream, n_streams * n_win, N, out, kw, (hipStream_t)stream, xm);
 }
 
 int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit) {
@@ -1211,7 +1238,7 @@ int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void*
   DeviceGuard dg(h->device);
   const int T = 1 + N / HOP;
   StftArgs sa{};
-  sa.B = B; sa.N = N; sa.ldx = N; sa.T = T; sa.Tp = round_up(T, TILE); sa.x = x;
+  sa.B = B; sa.N = N; sa.ldx = N; sa.T = T; sa.Tp = round_up(T, TILE); sa.x = x; sa.nstr = B; sa.hopw = 0;
   sa.window = h->P(h->win_out); sa.tw = (const float2*)h->P(h->tw);
   sa.Xout = (float2*)X; sa.spec_out = h->same_stft_window ? spec : nullptr;
   HIPCHK(launch_stft(sa, (hipStream_t)stream));
@@ -1240,10 +1267,31 @@ int32_t sepvad_pit_l1(const float* est, int64_t est_ld, const float* ref, int64_
   PitArgs a{};
   a.B = B; a.L = L; a.est = est; a.est_ld = est_ld; a.ref = ref; a.ref_ld = ref_ld;
   a.nblk = (int)std::min<long long>(PIT_MAX_BLOCKS, std::max<long long>(1, ((long long)B * L + 8191) / 8192));
-  static_assert(PIT_MAX_BLOCKS * 4 * sizeof(double) <= SEPVAD_PIT_SCRATCH_BYTES, "scratch size");
+  static_assert((PIT_MAX_BLOCKS + 1) * 4 * sizeof(double) <= SEPVAD_PIT_SCRATCH_BYTES, "scratch size");
   a.partial = (double*)scratch;
   a.perm_out = (long long*)perm_out; a.loss_out = loss_out; a.pw_out = pw_out;
   HIPCHK(launch_pit_l1(a, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_pit_l1_sums(const float* est, int64_t est_ld, const float* ref, int64_t ref_ld, int32_t B, int64_t L,
+                           void* scratch, double* sums, void* stream) {
+  if (!est || !ref || !scratch || !sums || B < 1 || L < 1 || est_ld < L || ref_ld < L)
+    return fail(SEPVAD_E_ARG, "sepvad_pit_l1_sums: bad arguments");
+  PitArgs a{};
+  a.B = B; a.L = L; a.est = est; a.est_ld = est_ld; a.ref = ref; a.ref_ld = ref_ld;
+  a.nblk = (int)std::min<long long>(PIT_MAX_BLOCKS, std::max<long long>(1, ((long long)B * L + 8191) / 8192));
+  a.partial = (double*)scratch;
+  HIPCHK(launch_pit_l1_sums(a, sums, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_pit_l1_choose(const double* sums, double count, int32_t B, int64_t* perm_out, float* loss_out,
+                             float* pw_out, void* stream) {
+  if (!sums || B < 1 || !(count > 0.0)) return fail(SEPVAD_E_ARG, "sepvad_pit_l1_choose: bad arguments");
+  PitArgs a{};
+  a.B = B; a.perm_out = (long long*)perm_out; a.loss_out = loss_out; a.pw_out = pw_out;
+  HIPCHK(launch_pit_l1_choose(a, sums, count, (hipStream_t)stream));
   return SEPVAD_OK;
 }
 

@@ -140,6 +140,8 @@ constexpr int GATE_ROWS = 16;
 
 struct StftArgs {
   int B, N, ldx, T, Tp;
+  int nstr;              // utterance u reads x + (u % nstr) * ldx + (u / nstr) * hopw: nstr = B, hopw = 0 for a
+  long long hopw;        // plain batch; streaming windows: u = window * nstr + stream (sepvad_forward_windows)
   const float* x;        // [B][ldx] (row stride ldx >= N: streaming windows are strided views)
   const float* window;   // [512]
   const float2* tw;      // [512] e^{-2 pi i m / 512}
@@ -200,6 +202,8 @@ struct AppendArgs {
   float* dst; long long dst_ld, d0;
 };
 hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s);
+hipError_t launch_pit_l1_sums(const PitArgs& a, double* sums, hipStream_t s);     // partials -> sums[4] (fixed order)
+hipError_t launch_pit_l1_choose(const PitArgs& a, const double* sums, double count, hipStream_t s);
 hipError_t launch_stream_append(const AppendArgs& a, hipStream_t s);
 
 // input preprocessing (prep.hip)

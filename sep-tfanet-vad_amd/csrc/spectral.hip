@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x, f0 = blockIdx.y * FR_PER_WG;
   for (int i = tid; i < 512; i += 256) tw[i] = a.tw[i];
-  const float* xb = a.x + (size_t)b * a.ldx;
+  const float* xb = a.x + (size_t)(b % a.nstr) * a.ldx + (size_t)(b / a.nstr) * a.hopw;
   const int N = a.N;
   constexpr int NR = FR_PER_WG / 4;
   // all of this wave's input samples first (frames f0 + 4 round + wave), so the loads of the four

@@ -1,5 +1,5 @@
 // Streaming-wrapper kernels (reference model/online_class_unknown_targets.py:72-105):
-//   k_pit_l1_partial / k_pit_l1_final  PITLossWrapper(nn.L1Loss(), pit_from="pw_pt") with
+//   k_pit_l1_partial / k_pit_l1_sums / k_pit_l1_choose  PITLossWrapper(nn.L1Loss(), pit_from="pw_pt") with
 //       return_incides=True (model/pit_wrapper.py:77-140,149-177,261-312): pairwise L1 losses between
 //       the new window's overlap region and the stitched signal's tail. nn.L1Loss() reduces over the
 //       batch AND the samples, so every pairwise loss is one scalar shared by the whole batch and the
@@ -9,7 +9,7 @@
 //       hop of every window lands in its slot of the preallocated stitched signal (no torch.cat).
 // Layouts: signals are [B][2][ld] fp32 (speaker rows with stride ld). HBM-bound, no MFMA.
 // Reductions are deterministic: fixed per-block ranges, per-block partials in double, summed in
-// block order by the finalizer.
+// block order by k_pit_l1_sums; a sharded stream batch all-reduces those 4 sums before k_pit_l1_choose.
 #include "device_common.h"
 
 namespace sepvad {
@@ -39,14 +39,23 @@ __global__ __launch_bounds__(PIT_THREADS) void k_pit_l1_partial(PitArgs a) {
   block_reduce_store<4>(acc, red, a.partial + (size_t)blockIdx.x * 4);
 }
 
-// One block: pairwise means, the permutation loss set (einsum over one-hot perms / n_src,
-// model/pit_wrapper.py:289-300), torch.min's first-minimum choice (:308), the indices (:311).
-__global__ __launch_bounds__(64) void k_pit_l1_final(PitArgs a, int nblk) {
+// The pairwise L1 sums of this launch's rows: block partials summed in block order (sums[4], double)
+__global__ __launch_bounds__(64) void k_pit_l1_sums(PitArgs a, int nblk, double* sums) {
   if (threadIdx.x != 0) return;
   double pw[4] = {0.0, 0.0, 0.0, 0.0};
   for (int k = 0; k < nblk; ++k)
     for (int j = 0; j < 4; ++j) pw[j] += a.partial[(size_t)k * 4 + j];
-  const double cnt = (double)a.B * (double)a.L;
+  for (int j = 0; j < 4; ++j) sums[j] = pw[j];
+}
+
+// One block: pairwise means from the sums (of this device's rows, or all-reduced over the ranks of a
+// sharded stream batch: nn.L1Loss means over the WHOLE batch, model/pit_wrapper.py:172-177), the permutation
+// loss set (einsum over one-hot perms / n_src, :289-300), torch.min's first-minimum choice (:308), the
+// indices (:311) for this device's a.B rows.
+__global__ __launch_bounds__(64) void k_pit_l1_choose(PitArgs a, const double* sums, double cnt) {
+  if (threadIdx.x != 0) return;
+  double pw[4];
+  for (int j = 0; j < 4; ++j) pw[j] = sums[j];
   float m[4];
   for (int j = 0; j < 4; ++j) m[j] = (float)(pw[j] / cnt);
   // pwl = pw^T (targets x estimates); perms (0,1), (1,0)
@@ -64,11 +73,24 @@ __global__ __launch_bounds__(64) void k_pit_l1_final(PitArgs a, int nblk) {
     for (int j = 0; j < 4; ++j) a.pw_out[j] = m[j];
 }
 
-hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s) {
+hipError_t launch_pit_l1_sums(const PitArgs& a, double* sums, hipStream_t s) {
   if (a.B < 1 || a.L < 1 || a.nblk < 1 || a.nblk > PIT_MAX_BLOCKS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_pit_l1_partial, dim3(a.nblk), dim3(PIT_THREADS), 0, s, a);
-  hipLaunchKernelGGL(k_pit_l1_final, dim3(1), dim3(64), 0, s, a, a.nblk);
+  hipLaunchKernelGGL(k_pit_l1_sums, dim3(1), dim3(64), 0, s, a, a.nblk, sums);
   return hipGetLastError();
+}
+
+hipError_t launch_pit_l1_choose(const PitArgs& a, const double* sums, double count, hipStream_t s) {
+  hipLaunchKernelGGL(k_pit_l1_choose, dim3(1), dim3(64), 0, s, a, sums, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s) {
+  // the sums live in the scratch right after the block partials
+  double* sums = a.partial + (size_t)PIT_MAX_BLOCKS * 4;
+  hipError_t e = launch_pit_l1_sums(a, sums, s);
+  if (e != hipSuccess) return e;
+  return launch_pit_l1_choose(a, sums, (double)a.B * (double)a.L, s);
 }
 
 // dst[b][i][d0 + n] = src[b][perm[b][i]][s0 + n], n < H  (perm null = identity)

@@ -22,6 +22,7 @@ PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVA
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
+    "sepvad_forward_windows", "sepvad_pit_l1_sums", "sepvad_pit_l1_choose",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
     "sepvad_stft", "sepvad_istft",
     "sepvad_pit_l1", "sepvad_stream_append",
@@ -79,6 +80,13 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_forward_strided.restype = i32
     lib.sepvad_forward_strided.argtypes = [P, P, ctypes.c_int64, i32, i32, ctypes.POINTER(SepVadOutputs),
                                            ctypes.POINTER(SepVadInferKw), P]
+    lib.sepvad_forward_windows.restype = i32
+    lib.sepvad_forward_windows.argtypes = [P, P, ctypes.c_int64, i32, i32, ctypes.c_int64, i32,
+                                           ctypes.POINTER(SepVadOutputs), ctypes.POINTER(SepVadInferKw), P]
+    lib.sepvad_pit_l1_sums.restype = i32
+    lib.sepvad_pit_l1_sums.argtypes = [P, ctypes.c_int64, P, ctypes.c_int64, i32, ctypes.c_int64, P, P, P]
+    lib.sepvad_pit_l1_choose.restype = i32
+    lib.sepvad_pit_l1_choose.argtypes = [P, ctypes.c_double, i32, P, P, P, P]
     lib.sepvad_set_split.restype = i32
     lib.sepvad_set_split.argtypes = [P, i32]
     lib.sepvad_set_fused.restype = i32
@@ -278,6 +286,27 @@ class Handle:
         if return_aux:
             res.update(spectrum=spectrum, masks_b=masks_b, mask_per_speaker=mask)
         return res
+
+    def forward_windows(self, x: torch.Tensor, n_win: int, hop: int, N: int, inference_kw=None):
+        """Every streaming window in ONE forward (sepvad_forward_windows): window k of row b of x [B, L]
+        starts at sample k * hop; returns sep [n_win, B, num_spk, N] (window-major). No est is produced."""
+        if x.device.type != "cuda" or x.dtype != torch.float32 or x.stride(-1) != 1:
+            raise RuntimeError("forward_windows: x must be a float32 ROCm tensor with unit sample stride")
+        B = x.shape[0]
+        S = self.cfg["num_spk"]
+        T = 1 + N // (self.cfg["n_fftBins"] // 2)
+        sep = torch.empty(n_win, B, S, N, device=self.device, dtype=torch.float32)
+        has_vad = bool(self.cfg["final_vad"]) and (not self.cfg["final_vad_masked_speakers"] or self.cfg["noisy_phase"])
+        vad = torch.empty(n_win * B, S, T, device=self.device, dtype=torch.float32) if has_vad else None
+        outs = SepVadOutputs(_ptr(sep).value, _ptr(vad).value, 0, 0, 0, 0)
+        kw = make_kw(inference_kw)
+        ld = x.stride(0) if B > 1 else x.shape[1]
+        _check(self._lib.sepvad_forward_windows(self._h, _ptr(x), ld, B, n_win, hop, N, ctypes.byref(outs),
+                                                ctypes.byref(kw) if kw is not None else None, self._stream()),
+               "sepvad_forward_windows")
+        if CHECK_EACH_FORWARD:
+            self.fused_status()
+        return sep
 
     def side_outputs(self, stream: int, B: int, T: int, want=("spectrum", "masks_b", "mask_per_speaker")):
         """The side attributes of the last forward on `stream` (sepvad_side_outputs), materialised now on that

@@ -7,8 +7,9 @@ full forward per window, matches the new window's speakers to the stitched outpu
 class keeps that algorithm, its attributes and its file outputs, and moves the data path onto the
 device:
 
-* windows are strided views of the (padded) input handed to ``sepvad_forward_strided`` — no
-  gather copy (``get_truncated_signal``, :39-41);
+* all windows of all streams run as ONE forward (``sepvad_forward_windows``): window k of stream b is read at
+  x + b * row + k * hop, no gather copy (``get_truncated_signal``, :39-41); only the PIT-L1 + append chain
+  is sequential over windows;
 * the stitched signal is one preallocated ``[B, 2, n_windows * hop]`` buffer; the reorder + append
   of each hop is one ``sepvad_stream_append`` launch (``reorder_source_mse`` + ``update_online_signal``,
   :28-37, :93-94); the permutation comes from ``sepvad_pit_l1`` and never leaves the device;
@@ -47,6 +48,7 @@ class OnlineSaving:
         self.reference_sisdr = []
         self.num_save_samples = 30
         self.similarity = False
+        self.one_forward = True  # all windows in one forward when possible (False: the reference's window loop)
         if criterion_similarity is not None:
             self.similarity = True
             self.criterion_similarity = criterion_similarity
@@ -108,8 +110,26 @@ class OnlineSaving:
         n = max(n_samples, self.fs * self.max_len)
         return int(np.floor((n - self.fs * self.max_len) / (self.fs * self.save_sec))) + 1
 
-    def calc_online(self, full_signal_mix, name_folder, sample_indx, inference_kw):
-        """Reference :72-105. Leaves the stitched signal in ``self.online_signal`` ([B, 2, n*hop])."""
+    def _batched_ok(self, n_total: int, n_win: int, hop: int, save: bool) -> bool:
+        """The one-forward path needs the native model, no per-window wav writes, and window offsets that
+        are exactly k * hop (the reference's float expression floor(fs * k * save_sec), :39-41)."""
+        if save or not self.one_forward or not hasattr(self.model, "native_handle"):
+            return False
+        return all(int(np.floor(self.fs * k * self.save_sec)) == k * hop for k in range(n_win))
+
+    def calc_online(self, full_signal_mix, name_folder, sample_indx, inference_kw, process_group=None):
+        """Reference :72-105. Leaves the stitched signal in ``self.online_signal`` ([B, 2, n*hop]).
+
+        Every window of every stream runs in ONE forward (``sepvad_forward_windows``, window-major: window k of
+        all streams is one contiguous block); only the PIT-L1 choice + append chain is sequential over windows
+        (two small launches per window). With per-window wav writes (sample_indx < num_save_samples) or a
+        non-native model the reference's window loop runs instead (same results). The model's side
+        attributes are not updated by the one-forward path (the reference leaves the last window's there).
+
+        process_group: streams sharded over ranks (bench.py cfg 3): the reference's PIT is batch-global
+        (nn.L1Loss means over the batch, model/pit_wrapper.py:172-177), so each window's 4 pairwise L1 sums
+        are all-reduced over the group (pit.pit_l1_sharded) and the sharded result equals the unsharded one.
+        """
         win = self.fs * self.max_len
         if full_signal_mix.shape[-1] < win:
             full_signal_mix = torch.nn.functional.pad(full_signal_mix, (0, win - full_signal_mix.shape[-1]))
@@ -121,10 +141,26 @@ class OnlineSaving:
         buf = torch.empty(B, 2, n_win * hop, dtype=torch.float32, device=dev)
         filled = 0
         save = sample_indx < self.num_save_samples
-        while self.indx <= max_indx:
-            truncated_signal_mix = self.get_truncated_signal(full_signal_mix)
+        total_rows = B
+        if process_group is not None:
+            import torch.distributed as dist
+            t = torch.tensor([B], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=process_group)
+            total_rows = int(t.item())
+        batched = self._batched_ok(full_signal_mix.shape[-1], n_win, hop, save)
+        if batched:
+            x = full_signal_mix.to(torch.float32)
+            if x.stride(-1) != 1:
+                x = x.contiguous()
             with torch.no_grad():
-                pred_separation, _, _ = self.model(truncated_signal_mix, inference_kw)
+                sep_w = self.model.native_handle(dev).forward_windows(x, n_win, hop, win, inference_kw)
+        while self.indx <= max_indx:
+            if batched:
+                pred_separation = sep_w[self.indx]
+            else:
+                truncated_signal_mix = self.get_truncated_signal(full_signal_mix)
+                with torch.no_grad():
+                    pred_separation, _, _ = self.model(truncated_signal_mix, inference_kw)
             L = pred_separation.shape[-1]
             # the reference seeds online_signal with the un-reordered last hop at indx 0 (:85-86)
             online = pred_separation[:, :, L - hop:] if self.indx == 0 else buf[:, :, :filled]
@@ -133,7 +169,10 @@ class OnlineSaving:
             ob, oe = _slice_bounds(n_on, -win + hop, None)                # :88
             pred_sim = pred_separation[:, :, pb:pe]
             online_sim = online[:, :, ob:oe]
-            _, batch_indices = self.criterion_similarity(pred_sim, online_sim, return_incides=True)
+            if process_group is not None:
+                _, batch_indices, _ = _pit.pit_l1_sharded(pred_sim, online_sim, total_rows, process_group)
+            else:
+                _, batch_indices = self.criterion_similarity(pred_sim, online_sim, return_incides=True)
             # reorder_source_mse + update_online_signal (:92-94) in one device launch
             d0 = 0 if self.indx == 0 else filled
             _pit.stream_append(pred_separation, L - hop, hop, batch_indices, buf, d0)

@@ -20,7 +20,7 @@ from torch import nn
 
 from . import native as _native
 
-PIT_SCRATCH_BYTES = 16384  # SEPVAD_PIT_SCRATCH_BYTES (include/sepvad.h)
+PIT_SCRATCH_BYTES = 16448  # SEPVAD_PIT_SCRATCH_BYTES (include/sepvad.h)
 _scratch = {}
 
 
@@ -66,6 +66,32 @@ def pit_l1(est: torch.Tensor, ref: torch.Tensor):
     rc = lib.sepvad_pit_l1(_native._ptr(est), eld, _native._ptr(ref), rld, B, L, _native._ptr(_scratch_for(dev)),
                            _native._ptr(perm), _native._ptr(loss), _native._ptr(pw), _stream(dev))
     _native._check(rc, "sepvad_pit_l1")
+    return loss, perm, pw
+
+
+def pit_l1_sharded(est: torch.Tensor, ref: torch.Tensor, total_rows: int, group=None):
+    """pit_l1 for a stream batch sharded over the ranks of `group` (total_rows streams over all ranks): the 4
+    pairwise L1 sums of this rank's rows (sepvad_pit_l1_sums) are all-reduced (one 32-byte RCCL all-reduce,
+    stream-ordered, no host sync), then every rank makes the batch-global choice of the unsharded call
+    (sepvad_pit_l1_choose) with count = total_rows * L."""
+    import torch.distributed as dist
+    lib = _native.load_library()
+    est, eld = _rows(est.float())
+    ref, rld = _rows(ref.float())
+    B, _, L = est.shape
+    dev = est.device
+    buf = torch.empty(4, dtype=torch.float64, device=dev)
+    rc = lib.sepvad_pit_l1_sums(_native._ptr(est), eld, _native._ptr(ref), rld, B, L, _native._ptr(_scratch_for(dev)),
+                                _native._ptr(buf), _stream(dev))
+    _native._check(rc, "sepvad_pit_l1_sums")
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    count = float(total_rows) * float(L)
+    perm = torch.empty(B, 2, dtype=torch.int64, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    pw = torch.empty(2, 2, dtype=torch.float32, device=dev)
+    rc = lib.sepvad_pit_l1_choose(_native._ptr(buf), count, B, _native._ptr(perm), _native._ptr(loss), _native._ptr(pw),
+                                  _stream(dev))
+    _native._check(rc, "sepvad_pit_l1_choose")
     return loss, perm, pw
 
 

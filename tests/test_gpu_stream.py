@@ -98,3 +98,51 @@ def test_wav_outputs_written_for_first_samples(net, tmp_path):
     assert (tmp_path / "utt" / "indx_2" / "mixed.wav").exists()
     sr, on0 = wavfile.read(str(tmp_path / "utt" / "online_signal0.wav"))
     assert sr == 16000 and np.array_equal(on0, ons.online_signal[0, 0].cpu().numpy())
+
+
+def test_one_forward_equals_window_loop(net, tmp_path):
+    """All windows in one forward (sepvad_forward_windows) == the reference's window loop (one forward per
+    window), bitwise: kernels are batch-invariant and the PIT chain sees the same inputs."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(5, 64000, 4100)[0]).to(DEV)
+    outs = []
+    for one in (True, False):
+        ons = pkg.OnlineSaving(net, str(tmp_path), _criterion())
+        ons.save_sec = 0.16
+        ons.one_forward = one
+        ons.calc_online(x, "s", 10 ** 6, dict(pkg.INFERENCE_KW_DEFAULTS))
+        outs.append(ons.online_signal.clone())
+    assert outs[0].shape == (5, 2, 7 * 2560)
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_pit_sums_decompose_over_shards():
+    """What a sharded stream batch does per window (pit_l1_sharded): the 4 pairwise L1 sums of each shard,
+    summed (the all-reduce), then the batch-global choice == the unsharded sepvad_pit_l1 (same permutation,
+    loss within double-rounding of the shard grouping)."""
+    import ctypes
+    from sep_tfanet_vad_amd import native, pit
+    lib = native.load_library()
+    g = torch.Generator().manual_seed(5)
+    ref = torch.randn(9, 2, 3000, generator=g)
+    est = ref.flip(1) + 0.3 * torch.randn(9, 2, 3000, generator=g)
+    est[:4] = ref[:4] + 0.3 * torch.randn(4, 2, 3000, generator=g)   # 4 streams prefer identity, 5 swap
+    est, ref = est.to(DEV), ref.to(DEV)
+    loss, perm, pw = pit.pit_l1(est, ref)
+    sums = torch.zeros(4, dtype=torch.float64, device=DEV)
+    for lo, hi in ((0, 4), (4, 9)):
+        part = torch.empty(4, dtype=torch.float64, device=DEV)
+        e, r = est[lo:hi].contiguous(), ref[lo:hi].contiguous()
+        rc = lib.sepvad_pit_l1_sums(native._ptr(e), e.stride(1), native._ptr(r), r.stride(1), hi - lo, 3000,
+                                    native._ptr(pit._scratch_for(est.device)), native._ptr(part),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        native._check(rc, "sepvad_pit_l1_sums")
+        sums += part
+    perm2 = torch.empty(9, 2, dtype=torch.int64, device=DEV)
+    loss2 = torch.empty((), dtype=torch.float32, device=DEV)
+    rc = lib.sepvad_pit_l1_choose(native._ptr(sums), 9.0 * 3000, 9, native._ptr(perm2), native._ptr(loss2), None,
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    native._check(rc, "sepvad_pit_l1_choose")
+    assert torch.equal(perm, perm2)
+    assert abs(loss.item() - loss2.item()) <= 1e-6 * abs(loss.item())
