@@ -1,6 +1,7 @@
 """Throughput of the MI355X Sep-TFAnet^VAD forward path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f16x3|fp32|bf16|f16] [--workload offline|stream]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f16x3|fp32|bf16|f16]
+                    [--workload offline|cfg4|cfg5|stream]
 
 One step = one ``SeparationModel.forward`` (config_with_vad.json) over a resident batch of 64
 synthetic 2-speaker mixtures of 32 000 samples (4 s @ 8 kHz resampled to 16 kHz by the
@@ -223,8 +224,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=B_PER_GPU, help="utterances per GPU per step")
-    ap.add_argument("--samples", type=int, default=N_SAMPLES)
+    ap.add_argument("--batch", type=int, default=None, help="utterances per GPU per step (default: the workload's)")
+    ap.add_argument("--samples", type=int, default=None)
     ap.add_argument("--split", type=int, default=DEFAULT_SPLIT,
                     help="concurrent utterance chunks per forward (internal streams; bitwise-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -232,8 +233,10 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32", "bf16", "f16"],
                     help="GEMM arithmetic: f16x3 / fp32 meet the fp32 parity gates (default f16x3); bf16 / f16 are "
                          "the reduced-precision arms (BASELINE cfg 2 / cfg 5; tolerance in DESIGN.md §4)")
-    ap.add_argument("--workload", default="offline", choices=["offline", "stream"],
-                    help="offline: cfg 2 (default, the BASELINE metric); stream: cfg 3 streaming wrapper")
+    ap.add_argument("--workload", default="offline", choices=["offline", "cfg4", "cfg5", "stream"],
+                    help="offline: cfg 2 (default, the BASELINE metric: B=64, N=32000); cfg4: 8 s reverberant "
+                         "mixtures, B=64/GPU, N=64000 (T=251); cfg5: B=128/GPU, N=32000 (run with --precision "
+                         "f16 for the fp16 arm); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
     rc = launch_ranks(args)
     if rc is not None:
@@ -257,10 +260,15 @@ def main():
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     net = net.eval().to(dev)
     net.native_precision = args.precision
-    B, N = args.batch, args.samples
+    B0, N0 = {"offline": (B_PER_GPU, N_SAMPLES), "cfg4": (64, 64000), "cfg5": (128, 32000)}[args.workload]
+    B = args.batch or B0
+    N = args.samples or N0
     T = 1 + N // 256
     # this rank's shard of utterances: global utterance ids [rank*B, (rank+1)*B)
-    x, _ = synth.make_batch(B, N, 10_000 + rank * B)
+    if args.workload == "cfg4":  # image-method reverberant mixtures (RT60 U[0.2, 0.6] s; host RIR generator)
+        x, _ = synth.make_reverb_batch(B, N, 40_000 + rank * B)
+    else:
+        x, _ = synth.make_batch(B, N, 10_000 + rank * B)
     x = torch.from_numpy(x).to(dev)
     h = net.native_handle(dev)
     h.reserve(B, N)
@@ -344,9 +352,13 @@ def main():
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
                     "recipe weights (pretrained .pth absent from the reference)",
             "config": {
-                "workload": f"cfg2 config_with_vad.json forward, B={B}/GPU, N={N} samples (4 s @ 8 kHz resampled "
-                            f"to 16 kHz), T={T} frames; full forward incl. STFT, 24 TCN blocks, VAD, iSTFT and "
-                            f"the reference's side outputs",
+                "workload": {"offline": f"cfg2 config_with_vad.json forward, B={B}/GPU, N={N} samples (4 s @ 8 kHz "
+                                        f"resampled to 16 kHz), T={T} frames",
+                             "cfg4": f"cfg4 config_with_vad.json forward on image-method reverberant mixtures, "
+                                     f"B={B}/GPU, N={N} samples (8 s @ 8 kHz), T={T} frames",
+                             "cfg5": f"cfg5 config_with_vad.json forward, B={B}/GPU, N={N} samples, T={T} "
+                                     f"frames, {args.precision} GEMMs"}[args.workload]
+                            + "; full forward: STFT, 24 TCN blocks, VAD, iSTFT, est (side attributes on read)",
                 "global_batch": world * B,
                 "seq_len": N,
                 "parallelism": f"dp{world} (independent utterance shards, no data-path collective)",
@@ -367,7 +379,7 @@ def main():
                 "gemm_share_of_forward": round(gemm_ms / tot_ms, 3) if tot_ms > 0 else None,
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "offline":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist is not None:
