@@ -19,6 +19,10 @@ Deliberate differences: the model and input live on the ROCm devi
 moves them); a non-16 kHz input is resampled and then normalised (the reference's resample branch hands
 a tensor to ``torch.from_numpy`` at :82 and raises). Spectrogram/VAD plots are not produced
 (visualisation is out of scope); ``save_vad`` writes the thresholded labels as ``.npy`` instead of PNGs.
+
+VAD saving follows the reference's condition ``config.resume == "model_without_vad.pth"`` (:96), where
+``config.resume`` is a ``pathlib.Path`` (parse_config.py:68-69) compared with a ``str``: never equal, so the
+reference never saves the VAD; ``run(..., save_vad_output=True)`` opts in explicitly.
 """
 from __future__ import annotations
 
@@ -138,7 +142,7 @@ def save_vad(vad_output, save_path):
 
 
 def run(config_path, resume, path_mix, save_test_path, online=True, precision_save=32, inference_kw=None,
-        device="cuda"):
+        device="cuda", save_vad_output=False):
     """only_inference.main (:27-97) for a config JSON (arch.args) and a checkpoint."""
     from scipy.io.wavfile import read
     from . import SeparationModel
@@ -157,8 +161,10 @@ def run(config_path, resume, path_mix, save_test_path, online=True, precision_sa
         OnlineSaving(model, save_test_path, crit).calc_online(x, "online_results", 0, ikw)
     with torch.no_grad():
         out_separation, output_vad, _ = model(x, ikw)
+    _ = model.mask_per_speaker  # the reference reads it for its mask plot (:92); plots are out of scope
     save_audio(x, out_separation, save_test_path, precision_save)
-    if isinstance(output_vad, torch.Tensor):
+    # only_inference.py:96: Path(resume) == "model_without_vad.pth" is always False (Path vs str)
+    if (save_vad_output or Path(resume) == "model_without_vad.pth") and isinstance(output_vad, torch.Tensor):
         save_vad(output_vad, save_test_path)
     return out_separation, output_vad
 

@@ -73,7 +73,12 @@ def test_cli_run_end_to_end(tmp_path, state_dicts):
     wavfile.write(str(tmp_path / "mix.wav"), 8000, (mix * 20000).astype(np.int16))
     out = tmp_path / "results"
     sep, vad = inference.run(str(cfg_path), str(ck), str(tmp_path / "mix.wav"), str(out), online=True,
-                             precision_save=32, inference_kw={"return_smoothed_vad": False}, device=DEV)
+                             precision_save=32, inference_kw={"return_smoothed_vad": False}, device=DEV,
+                             save_vad_output=True)
+    # the reference's own condition never saves the VAD (only_inference.py:96 compares a Path with a str)
+    out2 = tmp_path / "results_default"
+    inference.run(str(cfg_path), str(ck), str(tmp_path / "mix.wav"), str(out2), online=False, device=DEV)
+    assert (out2 / "Speaker_0.wav").exists() and not (out2 / "estimated_vad_0.npy").exists()
     assert tuple(sep.shape) == (1, 2, 40000)
     for f in ("Mixed_0.wav", "Speaker_0.wav", "Speaker_1.wav", "estimated_vad_0.npy"):
         assert (out / f).exists(), f
