@@ -75,8 +75,22 @@ def res_out_bytes(B, T):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r01m_pmc_tcn.json"      # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r02i_pmc_tcn.json"      # fused schedule (k_tcn)
 DEFAULT_SPLIT = 1
+
+
+def host_cores():
+    """CPU cores this process may use: the affinity set, capped by the cgroup CPU quota. On the GPU box
+    os.cpu_count() reports the whole machine while the job's share is 16 CPUs; threading to the machine
+    count there oversubscribes the share many times over."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def cpu_baseline(seconds: float = 12.0):
@@ -85,7 +99,7 @@ def cpu_baseline(seconds: float = 12.0):
     from oracle.torch_ref import OracleModel
     import sep_tfanet_vad_amd as pkg
     from sep_tfanet_vad_amd import synth
-    threads = os.cpu_count() or 1  # every host core, stated in the line
+    threads = host_cores()  # every core of this process's CPU share, stated in the line
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234).items()}
     om = OracleModel(pkg.CONFIG_WITH_VAD, sd, torch.float32)
@@ -97,11 +111,13 @@ def cpu_baseline(seconds: float = 12.0):
         om(xt)
         n_utt += B_PER_GPU
         el = time.perf_counter() - t0
+        print(f"cpu_baseline: {n_utt} utterances in {el:.1f} s", file=sys.stderr, flush=True)
         if el >= seconds and n_utt >= 2 * B_PER_GPU:
             break
     return dict(value=n_utt / el, unit="utterances/s", cores=threads, kind="port",
                 sample=f"{n_utt} utterances ({n_utt // B_PER_GPU} batches of B={B_PER_GPU}, N={N_SAMPLES}) "
-                       f"in {el:.1f} s, oracle/torch_ref.py fp32 on {threads} threads")
+                       f"in {el:.1f} s, oracle/torch_ref.py fp32 on {threads} threads (this process's CPU share: "
+                       f"affinity capped by the cgroup quota; os.cpu_count() = {os.cpu_count()})")
 
 
 def _free_port():
