@@ -88,10 +88,10 @@ class OracleModel:
         return self.sd[name].to(self.dtype)
 
     # ---- front end -------------------------------------------------------------------------
-    def stft(self, x):
-        """spec_input / spec_output (model/model.py:16-25,384-385,408-410), DC bin zeroed."""
+    def stft(self, x, window="spec_output.window"):
+        """spec_output / spec_input (model/model.py:16-25,384-385,408-410), DC bin zeroed."""
         n_fft = self.cfg["n_fftBins"]
-        win = self._t("spec_output.window")
+        win = self._t(window)
         X = torch.stft(x, n_fft, hop_length=n_fft // 2, win_length=n_fft, window=win, center=True,
                        pad_mode="reflect", normalized=False, onesided=True, return_complex=True)
         X = X.clone()
@@ -156,8 +156,11 @@ class OracleModel:
         N = x.shape[-1]
         F_ = cfg["n_fftBins"] // 2 + 1
         ns = cfg["num_spk"]
-        X = self.stft(x)                                          # [B,F,T] (both STFTs are identical)
-        power = X.abs() ** 2
+        X = self.stft(x)                                          # stft_out [B,F,T] (model/model.py:408)
+        Xin = X                                                   # stft (:409): the same unless the windows differ
+        if not torch.equal(self._t("spec_input.spec.window"), self._t("spec_output.window")):
+            Xin = self.stft(x, "spec_input.spec.window")
+        power = Xin.abs() ** 2
         spec = 10.0 * torch.log10(torch.clamp(power, min=1e-10))
         if cfg["activity_input_bool"]:
             g = F.conv2d(spec.unsqueeze(1), t("activity_input.weight"), t("activity_input.bias"), padding=1)

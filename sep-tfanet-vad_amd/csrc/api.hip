@@ -824,30 +824,27 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   const size_t g1_grid = (size_t)B * ntu * (CH / TILE);
   const bool probing = tr && h->probe && h->probe_blk >= 0;
 
-  // 1. STFT (spec_input for the spectrum, spec_output for est; identical windows -> one pass)
+  // 1+2. STFT (spec_output for est; spec_input for the spectrum: one transform when the windows are equal)
+  // fused with the activity gate, the TCN input and the TCN.LN statistics (k_stft_gate)
   {
     StftArgs sa{};
     sa.B = B; sa.N = N; sa.ldx = ldx; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
     sa.nstr = xm.nstr > 0 ? xm.nstr : B; sa.hopw = xm.nstr > 0 ? xm.hopw : 0;
     sa.window = h->P(h->win_out);
+    sa.window_db = h->same_stft_window ? sa.window : h->P(h->win_in);
     sa.X = w.X;
-    sa.specdb = h->same_stft_window ? w.specdb : nullptr;
-    HIPCHK(launch_stft(sa, s));
-    if (!h->same_stft_window) {
-      sa.window = h->P(h->win_in);
-      sa.X = nullptr;
-      sa.specdb = w.specdb;
-      HIPCHK(launch_stft(sa, s));
+    sa.specdb = h->same_stft_window ? nullptr : w.specdb;
+    sa.activity = c.activity_input; sa.gate_w = h->P(h->gate);
+    sa.S0 = w.S0; sa.gate_rec = w.rec_gate;
+    HIPCHK(launch_stft_gate(sa, s));
+    if (out->spectrum) {  // eager side output (Handle.forward(return_aux=True))
+      GateArgs ga{};
+      ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
+      ga.X = h->same_stft_window ? w.X : nullptr; ga.specdb = w.specdb; ga.w = h->P(h->gate);
+      ga.S0 = nullptr; ga.out_rec = nullptr;
+      ga.spec_side = out->spectrum + (size_t)b0 * NBIN * T;
+      HIPCHK(launch_gate(ga, s));
     }
-  }
-  // 2. activity gate + TCN.LN statistics
-  {
-    GateArgs ga{};
-    ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
-    ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = w.S0;
-    ga.spec_side = out->spectrum ? out->spectrum + (size_t)b0 * NBIN * T : nullptr;
-    ga.out_rec = w.rec_gate;
-    HIPCHK(launch_gate(ga, s));
   }
   // 3+4. TCN + output head
   const int G = (T + FR - 1) / FR;
@@ -1221,6 +1218,7 @@ int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* str
   if (out->spectrum) {  // the gated dB spectrum, recomputed from the dB spectrum (same arithmetic as k_gate)
     GateArgs ga{};
     ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = h->cfg.activity_input;
+    ga.X = h->same_stft_window ? w.X : nullptr;  // the dB spectrum from the stored STFT (or specdb)
     ga.specdb = w.specdb; ga.w = h->P(h->gate); ga.S0 = nullptr; ga.out_rec = nullptr;
     ga.spec_side = out->spectrum;
     HIPCHK(launch_gate(ga, s));

@@ -130,7 +130,8 @@ struct HeadStatsArgs {   // statistics of PReLU(o_final) for TCN.output.1
 
 struct GateArgs {
   int B, T, Tp, activity;
-  const float* specdb;   // [B][Tp][SPEC_LD]
+  const float* specdb;   // [B][Tp][SPEC_LD] (used when X is null)
+  const float2* X;       // nullable [B][Tp][NBIN]: the dB spectrum recomputed from the stored STFT (side pass)
   const float* w;        // activity_input.weight [9] ; bias at w[9]; prelu at w[10]
   float* S0;             // [B][Tp][CH] gated bins 1..256 (nullable: side-output pass)
   float* spec_side;      // nullable [B][NBIN][T] (self.spectrum)
@@ -149,7 +150,15 @@ struct StftArgs {
   float2* Xout;          // nullable [B][NBIN][T] (debug entry)
   float* specdb;         // nullable [B][Tp][SPEC_LD]
   float* spec_out;       // nullable [B][NBIN][T] (debug entry)
+  // fused STFT + activity gate (k_stft_gate, the forward): window_db != window only when the checkpoint's
+  // spec_input and spec_output windows differ (then specdb keeps the dB spectrum for the side pass)
+  const float* window_db;
+  int activity;
+  const float* gate_w;   // activity_input.weight [9], bias [9], prelu [10]
+  float* S0;             // [B][Tp][CH] gated bins 1..256 (TCN input)
+  double* gate_rec;      // [B][Tp/GATE_ROWS][2] TCN.LN partial statistics
 };
+hipError_t launch_stft_gate(const StftArgs& a, hipStream_t s);
 
 constexpr int VAD_ROWS = 32;
 struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4) partial stats

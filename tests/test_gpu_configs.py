@@ -55,3 +55,28 @@ def test_cfg5_precision_sweep(precision, state_dicts):
     s_ref, v_ref, _ = om(torch.from_numpy(x))
     err = _check(sep.cpu().numpy(), vad.cpu().numpy(), s_ref.numpy(), v_ref.numpy())
     print(f"cfg5 {precision}: sep max-abs vs fp32 oracle {err:.2e}")
+
+
+def test_distinct_stft_windows(state_dicts):
+    """A checkpoint whose spec_input and spec_output windows differ (model/model.py:383-385,408-409): the
+    spectrum / TCN input use spec_input's window, est and the output use spec_output's. The fused front end
+    then runs two transforms per frame and keeps the dB spectrum for the side pass. vs the oracle."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    sd = dict(state_dicts["with_vad"])
+    n = torch.arange(512, dtype=torch.float32)
+    sd["spec_input.spec.window"] = 0.54 - 0.46 * torch.cos(2 * torch.pi * n / 512)  # periodic Hamming
+    x, _ = synth.make_batch(3, 20000, 5170)
+    net = _net("with_vad", {"with_vad": sd}, "f16x3")
+    with torch.no_grad():
+        sep, vad, _ = net(torch.from_numpy(x).to(DEV))
+    om = OracleModel(config_of("with_vad"), sd, torch.float32)
+    s_ref, v_ref, _ = om(torch.from_numpy(x))
+    _check(sep.cpu().numpy(), vad.cpu().numpy(), s_ref.numpy(), v_ref.numpy())
+    spec = net.spectrum.cpu().numpy()
+    sref = om.spectrum.numpy() if hasattr(om, "spectrum") else None
+    if sref is not None:
+        X = torch.stft(torch.from_numpy(x), 512, 256, 512, sd["spec_input.spec.window"], center=True,
+                       pad_mode="reflect", return_complex=True)
+        ok = (X.abs() > 1e-2).numpy()
+        assert np.abs(spec - sref)[ok].max() <= 1e-5 * np.abs(sref).max()
