@@ -921,19 +921,25 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         }
       }
     }
-    GemmArgs g{};
-    g.B = B; g.T = T; g.Tp = Tp; g.M = MOUT_PAD; g.Mreal = MOUT; g.K = CH; g.ldy = MOUT_PAD;
-    set_weights(h, g, h->wout);
-    g.ascale = h->out_sx;
-    g.bias = h->P(h->bo);
-    g.ld.mode = LD_PLAIN; g.ld.X = w.O[0];
-    g.ld.head = 1; g.ld.alpha_h = h->out_a;
-    g.ld.gh = gn_src(w.rec_hs, G, 2, 0, h->P(h->out_g), h->P(h->out_b), 1e-5f);
-    g.Y = w.masks; g.Yside = out->masks_b ? out->masks_b + (size_t)b0 * MOUT * T : nullptr;
+    // output head on the members' slices (k_head), then the eager masks_b copy if asked
+    HeadArgs ha{};
+    ha.B = B; ha.T = T; ha.Tp = Tp; ha.G = G; ha.prec = h->prec;
+    ha.Xfin = w.O[0]; ha.rec = w.rec_hs;
+    ha.g = h->P(h->out_g); ha.be = h->P(h->out_b); ha.alpha = h->out_a; ha.sx = h->out_sx;
+    ha.inv_ch = 1.0 / ((double)CH * T);
+    ha.wh = h->H(h->prec == PREC_BF16 ? h->wout.fbf : h->wout.fhi);
+    ha.wl = h->H(h->wout.flo);
+    ha.wscale = h->P(h->wout.scale); ha.bias = h->P(h->bo);
+    ha.masks = w.masks;
     if (ev()) return SEPVAD_E_HIP;
-    HIPCHK(launch_gemm(g, EP_BIAS_OUT, s));
+    HIPCHK(launch_head(ha, s));
     if (ev()) return SEPVAD_E_HIP;
     if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
+    if (out->masks_b) {
+      MaskSideArgs m{};
+      m.B = B; m.T = T; m.Tp = Tp; m.masks = w.masks; m.masks_b = out->masks_b + (size_t)b0 * MOUT * T;
+      HIPCHK(launch_mask_side(m, s));
+    }
   } else {
     // 3. TCN blocks
     int cur = 0;  // w.O[cur] holds the current block input o once the conv1d GEMM materialized it

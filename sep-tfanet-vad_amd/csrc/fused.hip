@@ -936,6 +936,89 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule. One workgroup per 32-frame slice of
+// an utterance (the k_tcn members' slices), 9 waves x 2 tiles of 32 output channels (576 = 18 tiles): A =
+// GN_out(PReLU(x')) of the slice into LDS once (statistics from k_tcn's per-member records, fixed order),
+// then each wave streams its tiles' weights from L2 in fragment order (wave_gemm) and stores its channels
+// of the masks rows. Replaces the 64x64-tiled head GEMM, which re-read x' for each of its 9 channel tiles.
+constexpr int HTHR = 576;
+template <int PRE>
+__global__ __launch_bounds__(HTHR) void k_head(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 Ahi[FR * LDX];
+  __shared__ __attribute__((aligned(16))) _Float16 Alo[PRE == PREC_F16X3 ? FR * LDX : 8];
+  __shared__ float hs[2][CH];
+  __shared__ double dred[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int u = blockIdx.x / a.G, g = blockIdx.x % a.G, t0 = g * FR;
+  // first tile's weight ring in flight with the x' loads and the statistics
+  const __amdgpu_buffer_rsrc_t wh = rsrc_of(a.wh), wl = rsrc_of(PRE == PREC_F16X3 ? a.wl : a.wh);
+  u32x4v rh[PD], rl[PD];
+  prefetch_w<PRE>(wh, wl, (wave * NS1 * 64 + lane) * 16, rh, rl);
+  // raw x' of the slice: 32 rows x 256 channels, thread-contiguous channels (coalesced 1 KB rows)
+  constexpr int NV = FR * CH / HTHR + 1;  // 15
+  float xv[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = tid + k * HTHR;
+    xv[k] = i < FR * CH ? a.Xfin[((size_t)u * a.Tp + t0) * CH + i] : 0.f;
+  }
+  if (tid < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in order
+    double s = 0.0;
+    for (int mm = 0; mm < a.G; ++mm) s += a.rec[((size_t)u * a.G + mm) * 2 + tid];
+    dred[tid] = s;
+  }
+  __syncthreads();
+  if (tid < CH) {
+    float mu, rs;
+    gn_moments_f(dred[0], dred[1], a.inv_ch, 1e-5f, mu, rs);
+    const float sc = rs * a.g[tid];
+    hs[0][tid] = sc;
+    hs[1][tid] = a.be[tid] - sc * mu;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = tid + k * HTHR;
+    if (i < FR * CH) {
+      const int r = i / CH, c = i % CH;
+      const float v = fmaf(prelu_f(xv[k], a.alpha), hs[0][c], hs[1][c]);
+      split_store<PRE>(Ahi, Alo, r * LDX + c, v * a.sx);
+    }
+  }
+  __syncthreads();
+  // two tiles per wave: channels [32 j, 32 j + 32), j = wave, wave + 9; the second tile's ring is
+  // issued before the first tile's stores
+  const int hl4 = 4 * (lane >> 5);
+  f32x16v acc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int j = wave + 9 * q;
+    const int voff = (j * NS1 * 64 + lane) * 16;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    wave_gemm<NS1, LDX, PRE>(acc[q], Ahi, Alo, wh, wl, voff, rh, rl, lane);
+    if (q == 0) prefetch_w<PRE>(wh, wl, ((j + 9) * NS1 * 64 + lane) * 16, rh, rl);
+    const int m = 32 * j + (lane & 31);
+    const float ws = a.wscale[m], bias = a.bias[m];
+    float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + m;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = fmaf(acc[q][r], ws, bias);
+  }
+}
+
+hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
+  if (a.G < 1 || a.G * FR > a.Tp) return hipErrorInvalidValue;
+  const dim3 grid(a.B * a.G);
+  switch (a.prec) {
+    case PREC_F16X3: hipLaunchKernelGGL(k_head<PREC_F16X3>, grid, dim3(HTHR), 0, s, a); break;
+    case PREC_F16: hipLaunchKernelGGL(k_head<PREC_F16>, grid, dim3(HTHR), 0, s, a); break;
+    case PREC_BF16: hipLaunchKernelGGL(k_head<PREC_BF16>, grid, dim3(HTHR), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 template <int PRE>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
   if constexpr (PRE == PREC_F16X3) {

@@ -293,6 +293,21 @@ struct TcnArgs {
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
+// Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
+// for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
+struct HeadArgs {
+  int B, T, Tp, G, prec;
+  const float* Xfin;     // [B][Tp][CH] TCN output x'
+  const double* rec;     // [B][G][2] (sum, sumsq) of PReLU(x') per k_tcn member
+  const float* g; const float* be;  // TCN.output.1 affine
+  float alpha;           // TCN.output.0 PReLU
+  float sx;              // range scale of the A operand (undone by wscale)
+  double inv_ch;         // 1 / (CH * T)
+  const __half* wh; const __half* wl;  // fragment-ordered W planes [MOUT_PAD/32][CH/16][64][8] (wl: F16X3 only)
+  const float* wscale; const float* bias;  // [MOUT_PAD]
+  float* masks;          // [B][Tp][MOUT_PAD]
+};
+hipError_t launch_head(const HeadArgs& a, hipStream_t s);
 int tcn_blocks_per_cu(int ln_mode, int prec);
 
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
