@@ -899,6 +899,14 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
         ta.probe = h->tprobe;
+        if (env_int("SEPVAD_TCN_PROBE_WARM", 0)) {  // diagnostics: an unprobed launch first (warm caches)
+          TcnArgs tw = ta;
+          tw.probe = nullptr;
+          HIPCHK(launch_tcn(tw, ngl * G, s));
+          cx->tsalt = (cx->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
+          if (cx->tsalt == 0) cx->tsalt = 1;  // (diagnostics: no wrap re-zeroing needed within one forward)
+          ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
+        }
       }
       if (ev()) return SEPVAD_E_HIP;
       HIPCHK(launch_tcn(ta, ngl * G, s));

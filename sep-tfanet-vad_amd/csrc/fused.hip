@@ -515,14 +515,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const float* pm = sm.prm;
       // this block's parameters: loads issued now (behind the already-landed weight prefetch), stored
       // into LDS after the conv1d GEMM
-      float4 pv[3];
+      // Unconditional buffer loads (bytes past the blob read 0): a conditionally initialised array here was
+      // promoted to LDS by hipcc (24 KB, a dispatch-packet read for the work-group size at kernel entry, and
+      // a load -> vmcnt(0) -> ds_write chain at the start of every block).
+      u32x4v pv[3];
       {
-        const float4* src = reinterpret_cast<const float4*>(a.prm + (size_t)bi * PB_SIZE);
+        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(uni(a.prm + (size_t)bi * PB_SIZE)), (short)0, PB_SIZE * 4, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int idx = tid + k * NTHR;
-          if (idx < PB_SIZE / 4) pv[k] = src[idx];
-        }
+        for (int k = 0; k < 3; ++k) pv[k] = __builtin_amdgcn_raw_buffer_load_b128(pr, (tid + k * NTHR) * 16, 0, 0);
       }
 #if TCN_EPI
       // the epilogue's per-channel values straight into registers (no LDS round trip, no barrier)
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int idx = tid + k * NTHR;
-          if (idx < PB_SIZE / 4) reinterpret_cast<float4*>(sm.prm)[idx] = pv[k];
+          if (idx < PB_SIZE / 4) reinterpret_cast<u32x4v*>(sm.prm)[idx] = pv[k];
         }
 #if TCN_EPI
         const float ws = ws1, bias = b1;  // block_sums' barrier below makes the blob visible to later phases
