@@ -54,6 +54,18 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_MOM5
 #define TCN_MOM5 1   // recursive-LN moment record from 5 per-thread row sums, channel weights applied once
 #endif
+#ifndef TCN_PFX
+#define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
+#endif
+#ifndef TCN_GNW
+#define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
+#endif
+#if TCN_GNW && !TCN_FMOM
+#error "TCN_GNW finishes the moments in float (gn_moments_f): it needs TCN_FMOM"
+#endif
+#ifndef TCN_SUB
+#define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)
+#endif
 #ifndef TCN_EPI
 #define TCN_EPI 1    // conv1d epilogue parameters from global into registers: no barrier before the epilogue
 #endif
@@ -75,6 +87,7 @@ struct TcnSmem {
   float vec[CH + 8];              // channel means / rowsum staging
   float yf[CH + 8];
   float mC[FR + 8], yt[FR + 8], at[FR];
+  float gmom[4];                  // GN1 {mean, rstd}, GN2 {mean, rstd} (TCN_GNW)
   float cs[FR][8];                // per-frame channel partial sums (8 channel slices)
   float csum[FR];                 // own per-frame channel sums
   float red[NMOM * 16];
@@ -235,6 +248,15 @@ __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_b
   }
 }
 
+// Ring entry s only (the burst above spread over a phase's rows: a CU's texture path takes one 1 KB wave load
+// per ~16 clocks, so 8 waves issuing the whole ring at once stall ~1 us on issue)
+template <int PRE>
+__device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
+                                            u32x4v (&rh)[PD], u32x4v (&rl)[PD], int s) {
+  rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
+  if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+}
+
 // One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
 // bf16 bits (BF16, round to nearest even) in the hi plane.
 template <int PRE>
@@ -327,6 +349,20 @@ __device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int l
   double s = 0.0;
   for (int mm = 0; mm < G; ++mm) s += gd[2 * mm + j];
   return double2{readlane_d(s, 0), readlane_d(s, 1)};
+}
+// GroupNorm {mean, rstd} from the statistic words polled by one wave: lane base + 4 mm + {0, 1, 2, 3} holds
+// member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane): the same
+// doubles, in the same order, as member_sums2 over the words in LDS.
+__device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, double inv, float eps, float& mu, float& rs) {
+  double s = 0.0, ss = 0.0;
+  for (int mm = 0; mm < G; ++mm) {
+    const int l = base + 4 * mm;
+    const unsigned a0 = __builtin_amdgcn_readlane(w, l), a1 = __builtin_amdgcn_readlane(w, l + 1);
+    const unsigned b0 = __builtin_amdgcn_readlane(w, l + 2), b1 = __builtin_amdgcn_readlane(w, l + 3);
+    s += __builtin_bit_cast(double, ((u64)a1 << 32) | a0);
+    ss += __builtin_bit_cast(double, ((u64)b1 << 32) | b0);
+  }
+  gn_moments_f(s, ss, inv, eps, mu, rs);
 }
 // Block sums of NV per-thread values (512 threads): waves by DPP, the 8 wave totals in double in wave
 // order by thread j < NV into out[j]. One barrier; callers barrier again before reading `out`.
@@ -563,7 +599,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (r < 4 && hl == 0 && tl < dil) gputf(s1 + GW_TOP + tl * CH + m, tag1, v, l2);
           if (r >= 12 && hl == 1 && tl >= FR - dil) gputf(s1 + GW_BOT + (tl - (FR - dil)) * CH + m, tag1, v, l2);
         }
+        if (TCN_SUB == 2) TPROBE(13);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H complete
+        if (TCN_SUB == 2) TPROBE(14);
         if (tid < 2) gputd(s1 + GW_STAT + 2 * tid, tag1, sm.dred[tid], l2);
       TPROBE(2);
       }
@@ -596,10 +634,18 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (hrow[k] >= 0) sm.H[hrow[k] * CH + hcol[k]] = p[k] != nullptr ? __builtin_bit_cast(float, v[k]) : 0.f;
+#if TCN_GNW
+        if (wave_s == NTHR / 64 - 1) {  // the GN1 pollers' wave: moments before the barrier
+          float mu, rs;
+          member_moments_w(v[4], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
+          if (lane == 0) { sm.gmom[0] = mu; sm.gmom[1] = rs; }
+        }
+#else
         if (sk >= 0) sm.gw[sk] = v[4];
+#endif
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
+        if (!TCN_PFX) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
@@ -610,6 +656,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // as gn_affine: no LDS round trip, no barrier)
         float sc, sh;
         {
+#if TCN_GNW
+          const float mu = sm.gmom[0], rs = sm.gmom[1];
+#else
           const double2 acc = member_sums2(sm.gw, G, lane);
           float mu, rs;
 #if TCN_FMOM
@@ -617,9 +666,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #else
           gn_moments(acc.x, acc.y, (double)CH * T, 1e-8f, mu, rs);
 #endif
+#endif
           sc = rs * pm[PB_G1 + c];
           sh = pm[PB_BE1 + c] - sc * mu;
         }
+        if (TCN_SUB == 1) TPROBE(13);
         float wv[2][4];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -630,6 +681,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float st[2] = {0.f, 0.f};
         // rows rh0-D .. rh0+15+D of this channel once into registers (GN1 applied, zero outside [0, T));
         // H holds rows -4..35, so every load is in bounds and issued unconditionally
+        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
         auto rows = [&](auto DC) {
           constexpr int D = decltype(DC)::value;
           float hv[FR / 2 + 2 * D];
@@ -644,6 +696,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
+            // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
+            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -666,6 +720,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           case 3: rows(std::integral_constant<int, 3>{}); break;
           default: rows(std::integral_constant<int, 4>{}); break;
         }
+        if (TCN_SUB == 1) TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
       }
@@ -683,7 +738,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
         unsigned v[1];
         gpoll<1>(p, tag2, v, a);
+#if TCN_GNW
+        if (wave_s == 0) {  // the GN2 pollers' wave: moments before the barrier (eps rescaled with d)
+          float mu, rs;
+          member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
+          if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
+        }
+#else
         if (tid < 4 * G) sm.gw[tid] = v[0];
+#endif
         __syncthreads();  // also: every wave is done reading d from LDS
       TPROBE(6);
       }
@@ -692,11 +755,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       {
         float fmu, frs;
         {
+#if TCN_GNW
+          fmu = sm.gmom[2]; frs = sm.gmom[3];
+#else
           const double2 acc = member_sums2(sm.gw, G, lane);  // every member's GN2 sums, member order
 #if TCN_FMOM
           gn_moments_f(acc.x, acc.y, a.inv_hid, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
 #else
           gn_moments(acc.x, acc.y, (double)HID * T, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
+#endif
 #endif
         }
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
@@ -720,8 +787,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
       }
       // ---- TF_Attention (model/model.py:182-208) ----
+      if (TCN_SUB == 3) TPROBE(13);
       if (tf) {
         __syncthreads();
+        if (TCN_SUB == 3) TPROBE(14);
         if (tid < FR) {  // P3 words: per-frame channel sums (a_t)
           float s = 0.f;
 #pragma unroll
@@ -893,19 +962,20 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
           kc[0] = rs * pm[PB_LNAG + m]; kc[1] = pm[PB_LNAB + m] - kc[0] * mu;
         }
-      TPROBE(13);
+      if (TCN_SUB == 0) TPROBE(13);
       }
       // next block's conv1d weights: in flight during the x' update
-      if (bi + 1 < a.nblk) {
-        const __half* wn = wb + WL::BLOCK;
-        prefetch_w<PRE>(rsrc_of(wn), rsrc_of(wn + WL::W1L), voff1, rh, rl);
-      }
-      TPROBE(14);
+      // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
+      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
+      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
+      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
+      if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;

@@ -7,7 +7,7 @@ mkdir -p var
 objs=$(ls sep-tfanet-vad_amd/csrc/build/*.o | grep -v '/fused.o$')
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-variable $flags \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-variable -mllvm -disable-promote-alloca-to-lds $flags \
       -c sep-tfanet-vad_amd/csrc/fused.hip -o var/fused_$name.o &
 done
 wait

@@ -3,6 +3,7 @@
 usage: SEPVAD_TCN_PROBE=/tmp/p.bin python bench.py --steps 1 --warmup 1 --no-cpu-baseline
        python tools/tcn_probe.py /tmp/p.bin
 """
+import os
 import sys
 
 import numpy as np
@@ -12,6 +13,12 @@ NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN
 # sub-phase stamps currently placed in fused.hip: slot 13 after the residual-LN affines (x' update
 # phase start), slot 14 after the next block's weight prefetch is issued
 SUB = [(13, 11, "x': moments->affines"), (14, 13, "x': prefetch issue"), (12, 14, "x': update+barrier")]
+if os.environ.get("TCN_SUB") == "1":  # library built with -DTCN_SUB=1: the stamps sit in the depthwise conv
+    SUB = [(13, 3, "dw: GN1 affine"), (14, 13, "dw: rows (conv, PReLU, split stores)"), (4, 14, "dw: GN2 block sums")]
+elif os.environ.get("TCN_SUB") == "2":  # in the conv1d epilogue
+    SUB = [(13, 1, "epi: rows (PReLU, H stores, halo words)"), (14, 13, "epi: GN1 block sums"), (2, 14, "epi: GN1 words")]
+elif os.environ.get("TCN_SUB") == "3":  # in the GN2 fold / row and frame sums
+    SUB = [(13, 6, "rs: GN2 fold + rowsum words"), (14, 13, "rs: barrier"), (7, 14, "rs: frame sums + COL words")]
 
 
 def main(path):
