@@ -148,6 +148,7 @@ struct sepvad_model {
   std::vector<std::unique_ptr<StreamCtx>> ctx;
   std::mutex mu;
   int res_B = 0, res_N = 0;     // sepvad_reserve hint: every context's workspace is sized at least this
+  unsigned long long* kprobe = nullptr;  // SEPVAD_TAIL_PROBE diagnostics: [workgroups][8]
   unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
   // timing
   bool timing = false;
@@ -1065,7 +1066,26 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     is.est_out = out->est ? (float2*)out->est + u2 * NBIN * T : nullptr;
     is.mask_out = out->mask ? out->mask + u2 * NBIN * T : nullptr;
     is.y = out->sep + u2 * N;
-    HIPCHK(launch_istft(is, s));
+    const char* tail_probe = getenv("SEPVAD_TAIL_PROBE");  // diagnostics: per-workgroup phase stamps
+    const size_t kp_n = 8192 * 8;
+    if (tail_probe && !h->kprobe) HIPCHK(hipMalloc(&h->kprobe, kp_n * sizeof(unsigned long long)));
+    if (tail_probe) {
+      HIPCHK(hipMemsetAsync(h->kprobe, 0, kp_n * sizeof(unsigned long long), s));
+      is.probe = h->kprobe;
+    }
+    HIPCHK(launch_istft_pair(is, s));
+    if (tail_probe) {  // synchronous dump: {grid x, grid y, slots} + stamps
+      const long long gx = B, gy = (T + 10) / 11;  // k_istft_pair's grid (IP_OWN = 11)
+      std::vector<unsigned long long> hp((size_t)gx * gy * 8);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(hp.data(), h->kprobe, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      if (FILE* f = fopen(tail_probe, "wb")) {
+        const long long hdr[3] = {gx, gy, 8};
+        fwrite(hdr, sizeof(hdr), 1, f);
+        fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+        fclose(f);
+      }
+    }
   }
   return SEPVAD_OK;
 }
@@ -1402,6 +1422,7 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
+  if (h->kprobe) (void)hipFree(h->kprobe);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);
   delete h;

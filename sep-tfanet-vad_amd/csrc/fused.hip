@@ -444,9 +444,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   }
   bool l2 = false;
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
-  const int m = 32 * wave + (lane & 31);            // this lane's output channel in both GEMMs
-  const int hl = lane >> 5;
-  auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * hl; };
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
   const int voff1 = (wave * NS1 * 64 + lane) * 16, voff2 = (wave * NS2 * 64 + lane) * 16;

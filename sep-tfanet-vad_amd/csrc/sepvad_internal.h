@@ -189,6 +189,7 @@ struct IstftArgs {
   float2* est_out;       // nullable [BS][NBIN][T]
   float* mask_out;       // nullable [BS][NBIN][T]
   float* y;              // [BS][N]
+  unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 
 // streaming wrapper (stream.hip)
@@ -325,5 +326,6 @@ hipError_t launch_mask_side(const MaskSideArgs& a, hipStream_t s);
 hipError_t launch_stft(const StftArgs& a, hipStream_t s);
 hipError_t launch_vad1(const Vad1Args& a, hipStream_t s);
 hipError_t launch_istft(const IstftArgs& a, hipStream_t s);
+hipError_t launch_istft_pair(const IstftArgs& a, hipStream_t s);  // the forward (est_mode 1, S = 2)
 
 }  // namespace sepvad
