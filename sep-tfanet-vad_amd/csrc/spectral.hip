@@ -10,79 +10,13 @@
 // FFT: a 512-point real transform = one 256-point complex transform of z[m] = x[2m] + i x[2m+1]
 // (radix-4 Stockham, 4 stages, one wave per transform in LDS) plus the split/merge twiddle step.
 #include "device_common.h"
+#include "fft_common.h"
 
 namespace sepvad {
 
-constexpr int M256 = 256;
 constexpr int FR_PER_WG = 16;   // STFT frames per workgroup (4 waves x 4 rounds)
 constexpr int IS_OWN = 15;      // iSTFT frames owned per workgroup (+1 halo frame computed)
 constexpr int IS_FR = IS_OWN + 1;
-
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
-
-// One radix-4 Stockham stage (stride Ns) of a 256-point transform, one wave (lane = j).
-// Twiddle W512^idx, idx in [0, 512). HALF: the table holds only W512^0..255 (W512^(x+256) = -W512^x).
-template <bool HALF>
-__device__ __forceinline__ float2 twid(const float2* tw, int idx) {
-  if constexpr (HALF) {
-    const float2 w = tw[idx & 255];
-    return idx < 256 ? w : make_float2(-w.x, -w.y);
-  } else {
-    return tw[idx];
-  }
-}
-
-template <bool INV, bool HALF = false>
-__device__ __forceinline__ void fft_stage(const float2* in, float2* out, const float2* tw, int lane, int Ns) {
-  const int j = lane;
-  const int k = j & (Ns - 1);
-  float2 v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = in[j + r * 64];
-  if (Ns > 1) {
-#pragma unroll
-    for (int r = 1; r < 4; ++r) {
-      float2 w = twid<HALF>(tw, 2 * ((r * k * (64 / Ns)) & 255));  // W_256^(r k 64/Ns) = W_512^(2 ...)
-      if (INV) w.y = -w.y;
-      v[r] = cmul(v[r], w);
-    }
-  }
-  const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
-  const float2 a2 = cadd(v[1], v[3]);
-  float2 a3 = csub(v[1], v[3]);
-  a3 = INV ? make_float2(-a3.y, a3.x) : make_float2(a3.y, -a3.x);
-  const int idxD = (j / Ns) * Ns * 4 + k;
-  out[idxD] = cadd(a0, a2);
-  out[idxD + Ns] = cadd(a1, a3);
-  out[idxD + 2 * Ns] = csub(a0, a2);
-  out[idxD + 3 * Ns] = csub(a1, a3);
-}
-
-// Orders this wave's LDS writes before its later LDS reads (the buffers of a transform belong to one
-// wave: no workgroup barrier is needed between its stages).
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// 256-point transform of one wave ping-ponging between its buffers b0 and b1 (4 stages: result back
-// in b0); the caller's buffers must be complete for this wave (wave_lds_sync or a barrier) on entry.
-template <bool INV, bool HALF = false>
-__device__ inline void fft256(float2* b0, float2* b1, const float2* tw, int lane) {
-  fft_stage<INV, HALF>(b0, b1, tw, lane, 1);
-  wave_lds_sync();
-  fft_stage<INV, HALF>(b1, b0, tw, lane, 4);
-  wave_lds_sync();
-  fft_stage<INV, HALF>(b0, b1, tw, lane, 16);
-  wave_lds_sync();
-  fft_stage<INV, HALF>(b1, b0, tw, lane, 64);
-  wave_lds_sync();
-}
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
@@ -571,262 +505,6 @@ __global__ __launch_bounds__(512) void k_istft(IstftArgs a) {
     }
     yb[n] = num / den;
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// In-place 256-point transform of one wave (radix-4 decimation in time, 4 stages): input at base-4
-// digit-reversed positions, output in natural order, each lane one butterfly per stage reading and writing
-// the same 4 positions (no second buffer). Same twiddles and butterfly as fft_stage.
-__device__ __forceinline__ int rev4(int n) {
-  return ((n & 3) << 6) | ((n & 12) << 2) | ((n & 48) >> 2) | ((n >> 6) & 3);
-}
-template <bool INV, bool HALF>
-__device__ __forceinline__ void fft256_inplace(float2* buf, const float2* tw, int lane) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int lq = 2 * s, Lq = 1 << lq;  // sub-transform length 1, 4, 16, 64
-    const int j = lane & (Lq - 1);
-    const int base = (lane >> lq) * (4 * Lq) + j;
-    float2 v[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) v[m] = buf[base + m * Lq];
-    if (s > 0) {
-#pragma unroll
-      for (int m = 1; m < 4; ++m) {
-        float2 w = twid<HALF>(tw, 2 * ((m * j * (64 / Lq)) & 255));  // W_{4Lq}^(j m) = W_512^(2 j m 64/Lq)
-        if (INV) w.y = -w.y;
-        v[m] = cmul(v[m], w);
-      }
-    }
-    const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
-    const float2 a2 = cadd(v[1], v[3]);
-    float2 a3 = csub(v[1], v[3]);
-    a3 = INV ? make_float2(-a3.y, a3.x) : make_float2(a3.y, -a3.x);
-    buf[base] = cadd(a0, a2);
-    buf[base + Lq] = cadd(a1, a3);
-    buf[base + 2 * Lq] = csub(a0, a2);
-    buf[base + 3 * Lq] = csub(a1, a3);
-    wave_lds_sync();
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// The forward's back end (est_mode 1): one workgroup (8 waves) per (utterance, chunk of IP_OWN frames) for
-// BOTH speakers, so each X row is read once for the two masks. Frames [f0-1, f0+IP_OWN) of both speakers:
-// 2 * IP_FR = 24 transforms, 3 rounds of 8 waves; owned output segments [f0, f0+IP_OWN) (+ segment T for
-// the last chunk). The transforms run in place in the frames' own LDS rows (fft256_inplace), so the
-// workgroup needs ~52 KB: three per CU, and at T = 126 the 64 x 12 workgroups of a B = 64 forward are all
-// resident at once (one round). Overlap-add: one reciprocal window envelope per thread (its sample phase q
-// is fixed across its segments), then products.
-constexpr int IP_OWN = 11;
-constexpr int IP_FR = IP_OWN + 1;
-#ifndef ISTFT_WAVES
-#define ISTFT_WAVES 6   // waves per SIMD the register budget must allow: 6 -> three 8-wave workgroups per CU
-#endif
-__global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
-  __shared__ float2 tw[256];
-  __shared__ float2 spec[2][IP_FR][NBIN + 1];  // est of the computed frames; transformed in place
-  __shared__ float yn[2][4][IP_FR + 6];   // GN'd VAD features, frames fbeg-3 .. fbeg+IP_FR+2
-  __shared__ float vadv[2][IP_FR + 4];    // vad at frames fbeg-2 .. fbeg+IP_FR+1
-  __shared__ float gain[2][IP_FR];
-  __shared__ float vs[2][4], vh[2][4];
-  __shared__ double dacc[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x, f0 = blockIdx.y * IP_OWN;
-  const int T = a.T;
-  const int fbeg = f0 - 1;
-  const bool vad = a.has_vad != 0;
-  // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
-  unsigned long long* const pr = a.probe ? a.probe + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
-  auto stamp = [&](int k) {
-    if (pr && tid == 0) pr[k] = __builtin_amdgcn_s_memtime();
-  };
-  if (pr && tid == 0) pr[0] = wall_clock64();
-  stamp(1);
-  if (tid < 256) tw[tid] = a.tw[tid];
-
-  // every input load first: X and both speakers' mask rows of the computed frames, the VAD features, the
-  // BN_1 records and parameters (frames outside [0, T) load a clamped row)
-  constexpr int NE = (IP_FR * NBIN + 511) / 512;
-  float2 xr[NE];
-  float mr[2][NE];
-#pragma unroll
-  for (int j = 0; j < NE; ++j) {
-    const int i = min(tid + j * 512, IP_FR * NBIN - 1);
-    const int fi = i / NBIN, k = i - fi * NBIN;
-    const size_t row = (size_t)b * a.Tp + min(max(fbeg + fi, 0), T - 1);
-    xr[j] = a.X[row * NBIN + k];
-    mr[0][j] = a.masks[row * MOUT_PAD + k];
-    mr[1][j] = a.masks[row * MOUT_PAD + NBIN + k];
-  }
-  constexpr int NQ = IP_FR + 6;
-  float yv = 0.f;
-  if (vad && tid < 2 * 4 * NQ) {  // thread -> (speaker, feature o, frame q)
-    const int sp = tid / (4 * NQ), o = (tid / NQ) % 4, q = tid % NQ;
-    const int fc = min(max(fbeg - 3 + q, 0), T - 1);
-    yv = a.vy[(((size_t)b * 2 + sp) * 4 + o) * a.Tp + fc];
-  }
-
-  // 1) X sigmoid(mask) of both speakers into the rows (frame-major, coalesced over bins); the VAD gain is
-  // applied when the rows are read (gain * (X m), the same product order as est = X m gain); noisy-phase
-  // synthesis (|X| m) e^{j angle X} == X m up to rounding (model/model.py:430-437)
-#pragma unroll
-  for (int j = 0; j < NE; ++j) {
-    const int i = tid + j * 512;
-    if (i < IP_FR * NBIN) {
-      const int fi = i / NBIN, k = i - fi * NBIN;
-      const int f = fbeg + fi;
-      const bool ok = f >= 0 && f < T;
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        const float m = ok ? sigmoid_f(mr[sp][j]) : 0.f;
-        spec[sp][fi][k] = ok ? make_float2(xr[j].x * m, xr[j].y * m) : make_float2(0.f, 0.f);
-      }
-    }
-  }
-  stamp(2);
-
-  // 0) VAD tail (model/model.py:160-179,444-457) for the frames of both speakers
-  if (vad) {
-    float g = 0.f, be = 0.f;
-    if (tid < 8) { g = a.vgn.g[tid & 3]; be = a.vgn.be[tid & 3]; }
-    reduce_records(rec_src(a.vgn, 2 * b, 2), rec_src(a.vgn, 2 * b + 1, 2), dacc);  // BN_1 = GroupNorm(1, 4)
-    lds_sync();
-    if (tid < 8) {
-      const int sp = tid >> 2, o = tid & 3;
-      float mu, rs;
-      gn_moments(dacc[2 * sp], dacc[2 * sp + 1], 4.0 * T, a.vgn.eps, mu, rs);
-      vs[sp][o] = rs * g;
-      vh[sp][o] = be - vs[sp][o] * mu;
-    }
-    lds_sync();
-    if (tid < 2 * 4 * NQ) {
-      const int sp = tid / (4 * NQ), o = (tid / NQ) % 4, qq = tid % NQ;
-      const int f = fbeg - 3 + qq;
-      yn[sp][o][qq] = (f >= 0 && f < T) ? fmaf(yv, vs[sp][o], vh[sp][o]) : 0.f;
-    }
-    lds_sync();
-    if (tid < 2 * (IP_FR + 4)) {
-      const int sp = tid / (IP_FR + 4), qq = tid % (IP_FR + 4);
-      const int f = fbeg - 2 + qq;
-      float z = a.b2;
-#pragma unroll
-      for (int o = 0; o < 4; ++o)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) z = fmaf(a.w2[o * 3 + k], yn[sp][o][qq + k], z);
-      const float p = sigmoid_f(z);
-      vadv[sp][qq] = (f >= 0 && f < T) ? p : 0.f;
-      if (!a.kw_enabled && f >= f0 && f < f0 + IP_OWN && f < T) a.vad_out[((size_t)b * 2 + sp) * T + f] = p;
-    }
-    lds_sync();
-    if (tid < 2 * IP_FR) {
-      const int sp = tid / IP_FR, fi = tid % IP_FR;
-      const int f = fbeg + fi;
-      float gg = 1.f;
-      if (a.kw_enabled && f >= 0 && f < T) {
-        auto thr = [&](int ff) -> float {  // threshold of frame ff (0 outside [0,T): zero padding)
-          if (ff < 0 || ff >= T) return 0.f;
-          return vadv[sp][ff - (fbeg - 2)] >= a.thr ? 1.f : 0.f;
-        };
-        float smv = fminf(thr(f - 1) + thr(f + 1), 1.f);
-        if (f == 0 || f == T - 1) smv = thr(f);
-        if (a.filt) gg = smv;
-        if (f >= f0 && f < f0 + IP_OWN)
-          a.vad_out[((size_t)b * 2 + sp) * T + f] = a.ret_smooth ? smv : vadv[sp][f - (fbeg - 2)];
-      }
-      gain[sp][fi] = gg;
-    }
-  } else {
-    if (tid < 2 * IP_FR) gain[tid / IP_FR][tid % IP_FR] = 1.f;
-  }
-  lds_sync();
-  stamp(3);
-
-  // side outputs of the owned frames, bin-major [bs][k][f] (IP_OWN consecutive frames per bin): est from the
-  // rows, sigmoid(mask) recomputed from the masks (read again: side path only)
-  if (a.est_out || a.mask_out) {
-    constexpr int NI = (2 * NBIN * IP_OWN + 511) / 512;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int i = tid + j * 512;
-      const int sp = i / (NBIN * IP_OWN), rem = i - sp * (NBIN * IP_OWN);
-      const int k = rem / IP_OWN, fo = rem - k * IP_OWN;
-      const int f = f0 + fo;
-      if (i < 2 * NBIN * IP_OWN && f < T) {
-        const size_t o = (((size_t)b * 2 + sp) * NBIN + k) * T + f;
-        if (a.est_out) {
-          const float2 e = spec[sp][fo + 1][k];
-          const float gg = gain[sp][fo + 1];
-          a.est_out[o] = make_float2(gg * e.x, gg * e.y);
-        }
-        if (a.mask_out) a.mask_out[o] = sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]);
-      }
-    }
-    lds_sync();  // the transforms below overwrite the rows
-  }
-  // 2) inverse real FFT of every computed frame in its own row: transform t = 8 round + wave
-  for (int t = wave; t < 2 * IP_FR; t += 8) {
-    float2* Y = spec[t / IP_FR][t % IP_FR];
-    const float gg = gain[t / IP_FR][t % IP_FR];
-    float2 zv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = lane + 64 * r;  // 0..255
-      const float2 y0 = Y[k], y1 = Y[M256 - k];
-      float2 yk = make_float2(gg * y0.x, gg * y0.y), ym = make_float2(gg * y1.x, gg * y1.y);
-      if (k == 0) { yk.y = 0.f; ym.y = 0.f; }  // c2r ignores Im of DC and Nyquist
-      const float2 cym = conjf2(ym);
-      const float2 E = make_float2(0.5f * (yk.x + cym.x), 0.5f * (yk.y + cym.y));
-      const float2 Dd = csub(yk, cym);
-      float2 w = tw[k];
-      w.y = -w.y;  // W512^{-k}
-      const float2 Oo = cmul(make_float2(0.5f * Dd.x, 0.5f * Dd.y), w);
-      zv[r] = make_float2(E.x - Oo.y, E.y + Oo.x);  // E + i O
-    }
-    wave_lds_sync();  // every lane's reads of the row done before it is overwritten
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Y[rev4(lane + 64 * r)] = zv[r];
-    wave_lds_sync();
-    fft256_inplace<true, true>(Y, tw, lane);
-    float* fr = reinterpret_cast<float*>(Y);  // time samples (pairs) in place
-    const float sc = 1.f / 256.f;             // 1/N of the 512-point c2r == 1/256 on the half-length transform
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = lane + 64 * r;
-      const float2 v = Y[m];
-      fr[2 * m] = v.x * sc * a.window[2 * m];
-      fr[2 * m + 1] = v.y * sc * a.window[2 * m + 1];
-    }
-  }
-  lds_sync();  // every frame's time samples in place for the overlap-add
-  stamp(4);
-  // 3) overlap-add of the owned segments, times the reciprocal window envelope (torch.istft)
-  const int q = tid & (HOP - 1);  // this thread's sample phase in every segment
-  const float wq0 = a.window[q], wq1 = a.window[q + HOP];
-  const int nseg = min(IP_OWN, T - f0) + ((f0 + IP_OWN >= T) ? 1 : 0);
-  const float inv_mid = 1.f / (wq0 * wq0 + wq1 * wq1);  // segments 1..T-1: frame j and frame j-1
-  const float inv_last = 1.f / (wq1 * wq1);             // segment T: frame T-1 only
-#pragma unroll
-  for (int sp = 0; sp < 2; ++sp) {
-    float* yb = a.y + ((size_t)b * 2 + sp) * a.N;
-    for (int i = tid; i < nseg * HOP; i += 512) {
-      const int j = f0 + i / HOP;
-      const int n = j * HOP + q - HOP;
-      if (n < 0 || n >= a.N) continue;  // segment 0 lies in the centre padding
-      float num = 0.f;
-      if (j < T) num += reinterpret_cast<const float*>(spec[sp][j - fbeg])[q];  // frame j, first half
-      num += reinterpret_cast<const float*>(spec[sp][j - 1 - fbeg])[q + HOP];    // frame j-1, second half
-      yb[n] = num * (j < T ? inv_mid : inv_last);
-    }
-  }
-  stamp(5);
-}
-
-hipError_t launch_istft_pair(const IstftArgs& a, hipStream_t s) {
-  if (a.S != 2 || a.BS % 2 || a.est_mode != 1) return hipErrorInvalidValue;
-  dim3 grid(a.BS / 2, (a.T + IP_OWN - 1) / IP_OWN);
-  hipLaunchKernelGGL(k_istft_pair, grid, dim3(512), 0, s, a);
-  return hipGetLastError();
 }
 
 hipError_t launch_istft(const IstftArgs& a, hipStream_t s) {
