@@ -811,6 +811,38 @@ struct XMap {
   long long hopw = 0;
 };
 
+// Diagnostics (SEPVAD_TAIL_PROBE=<prefix>): per-workgroup phase stamps of a tail kernel, dumped synchronously
+// to <prefix>.<kernel> as {grid x, grid y, 8} + [workgroups][8] (tools/tail_probe.py). Inactive otherwise.
+struct TailProbe {
+  static constexpr size_t N = 8192 * 8;
+  sepvad_model* h;
+  hipStream_t s;
+  std::string path;
+  unsigned long long* buf = nullptr;
+  TailProbe(sepvad_model* h_, hipStream_t s_, const char* kernel) : h(h_), s(s_) {
+    const char* pre = getenv("SEPVAD_TAIL_PROBE");
+    if (!pre) return;
+    path = std::string(pre) + "." + kernel;
+    if (!h->kprobe && hipMalloc(&h->kprobe, N * sizeof(unsigned long long)) != hipSuccess) return;
+    if (hipMemsetAsync(h->kprobe, 0, N * sizeof(unsigned long long), s) != hipSuccess) return;
+    buf = h->kprobe;
+  }
+  hipError_t dump(long long gx, long long gy) {
+    if (!buf) return hipSuccess;
+    std::vector<unsigned long long> hp((size_t)std::min<long long>(gx * gy * 8, (long long)N));
+    hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpy(hp.data(), buf, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    if (FILE* f = fopen(path.c_str(), "wb")) {
+      const long long hdr[3] = {gx, gy, 8};
+      fwrite(hdr, sizeof(hdr), 1, f);
+      fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+      fclose(f);
+    }
+    return hipSuccess;
+  }
+};
+
 int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b0, int B, int N,
                   const SepVadOutputs* out, const SepVadInferKw* kw, hipStream_t s, TimingRec* tr,
                   const XMap& xm) {
@@ -837,7 +869,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     sa.specdb = h->same_stft_window ? nullptr : w.specdb;
     sa.activity = c.activity_input; sa.gate_w = h->P(h->gate);
     sa.S0 = w.S0; sa.gate_rec = w.rec_gate;
+    TailProbe tp(h, s, "stft");
+    sa.probe = tp.buf;
     HIPCHK(launch_stft_gate(sa, s));
+    HIPCHK(tp.dump(B, Tp / (2 * GATE_ROWS)));  // k_stft_gate's grid (32 own frames)
     if (out->spectrum) {  // eager side output (Handle.forward(return_aux=True))
       GateArgs ga{};
       ga.B = B; ga.T = T; ga.Tp = Tp; ga.activity = c.activity_input;
@@ -1045,7 +1080,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     v.masks = w.masks; v.X = w.X;
     v.w1 = h->P(h->v_w1); v.b1 = h->P(h->v_b1); v.alpha = h->v_a;
     v.vy = w.vy; v.out_rec = w.rec_vad;
+    TailProbe tp(h, s, "vad1");
+    v.probe = tp.buf;
     HIPCHK(launch_vad1(v, s));
+    HIPCHK(tp.dump(B * 2, Tp / VAD_ROWS));
   }
   // 6. VAD tail + est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-460)
   {
@@ -1066,26 +1104,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     is.est_out = out->est ? (float2*)out->est + u2 * NBIN * T : nullptr;
     is.mask_out = out->mask ? out->mask + u2 * NBIN * T : nullptr;
     is.y = out->sep + u2 * N;
-    const char* tail_probe = getenv("SEPVAD_TAIL_PROBE");  // diagnostics: per-workgroup phase stamps
-    const size_t kp_n = 8192 * 8;
-    if (tail_probe && !h->kprobe) HIPCHK(hipMalloc(&h->kprobe, kp_n * sizeof(unsigned long long)));
-    if (tail_probe) {
-      HIPCHK(hipMemsetAsync(h->kprobe, 0, kp_n * sizeof(unsigned long long), s));
-      is.probe = h->kprobe;
-    }
+    TailProbe tp(h, s, "istft");
+    is.probe = tp.buf;
     HIPCHK(launch_istft_pair(is, s));
-    if (tail_probe) {  // synchronous dump: {grid x, grid y, slots} + stamps
-      const long long gx = B, gy = (T + 10) / 11;  // k_istft_pair's grid (IP_OWN = 11)
-      std::vector<unsigned long long> hp((size_t)gx * gy * 8);
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipMemcpy(hp.data(), h->kprobe, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      if (FILE* f = fopen(tail_probe, "wb")) {
-        const long long hdr[3] = {gx, gy, 8};
-        fwrite(hdr, sizeof(hdr), 1, f);
-        fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
-        fclose(f);
-      }
-    }
+    HIPCHK(tp.dump(B, (T + 10) / 11));  // k_istft_pair's grid (IP_OWN = 11)
   }
   return SEPVAD_OK;
 }

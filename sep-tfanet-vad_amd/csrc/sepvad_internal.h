@@ -157,6 +157,7 @@ struct StftArgs {
   const float* gate_w;   // activity_input.weight [9], bias [9], prelu [10]
   float* S0;             // [B][Tp][CH] gated bins 1..256 (TCN input)
   double* gate_rec;      // [B][Tp/GATE_ROWS][2] TCN.LN partial statistics
+  unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_stft_gate(const StftArgs& a, hipStream_t s);
 
@@ -170,6 +171,7 @@ struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4)
   float alpha;
   float* vy;             // [B][2][4][Tp]
   double* out_rec;       // [B*2][Tp/VAD_ROWS][2]
+  unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 
 struct IstftArgs {

@@ -107,116 +107,6 @@ hipError_t launch_stft(const StftArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// The forward's front end in one launch (model/model.py:408-419,421): STFT of GATE_ROWS own frames plus one
-// halo frame either side (recomputed, 18 transforms for 16 frames), X stored frame-major for the iSTFT, the
-// dB spectrum kept in LDS (never written to HBM unless the two STFT windows differ), then the activity gate
-// 3x3 conv + PReLU + multiply (the arithmetic of k_gate), the TCN input S0 and the TCN.LN partial records.
-constexpr int SG_FR = GATE_ROWS + 2;
-__global__ __launch_bounds__(256) void k_stft_gate(StftArgs a) {
-  __shared__ float2 tw[512];
-  __shared__ float2 work[4][2][M256];
-  __shared__ float S[SG_FR][NBIN + 2];   // dB of frames f0-1 .. f0+16 (zero outside [0, T)), bins -1 .. 257
-  __shared__ float red[2 * 16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x, f0 = blockIdx.y * GATE_ROWS;
-  const int T = a.T, N = a.N;
-  for (int i = tid; i < 512; i += 256) tw[i] = a.tw[i];
-  const float* xb = a.x + (size_t)(b % a.nstr) * a.ldx + (size_t)(b / a.nstr) * a.hopw;
-  constexpr int NR = (SG_FR + 3) / 4;  // rounds of 4 waves
-  // all of this wave's input samples first (frame fi = 4 round + wave, f = f0 - 1 + fi); frames outside
-  // [0, T) load frame 0 / T-1 (in bounds, unused)
-  float2 z[NR][4];
-#pragma unroll
-  for (int round = 0; round < NR; ++round) {
-    const int f = min(max(f0 - 1 + round * 4 + wave, 0), T - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = lane + 64 * r;
-      int s0 = f * HOP + 2 * m - HOP, s1 = s0 + 1;  // reflect padding of 256 on both sides
-      s0 = s0 < 0 ? -s0 : (s0 >= N ? 2 * (N - 1) - s0 : s0);
-      s1 = s1 < 0 ? -s1 : (s1 >= N ? 2 * (N - 1) - s1 : s1);
-      z[round][r] = make_float2(xb[s0], xb[s1]);
-    }
-  }
-  for (int i = tid; i < SG_FR; i += 256) { S[i][0] = 0.f; S[i][NBIN + 1] = 0.f; }
-  lds_sync();  // twiddles
-  const bool two = a.window_db != a.window;  // rare: distinct spec_input / spec_output windows
-#pragma unroll
-  for (int round = 0; round < NR; ++round) {
-    const int fi = round * 4 + wave, f = f0 - 1 + fi;
-    if (fi >= SG_FR) break;
-    const bool live = f >= 0 && f < T;
-    const bool own = live && fi >= 1 && fi <= GATE_ROWS;
-    for (int pass = 0; pass < (two ? 2 : 1); ++pass) {
-      const float* win = pass == 0 ? a.window : a.window_db;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = lane + 64 * r;
-        work[wave][0][m] = make_float2(win[2 * m] * z[round][r].x, win[2 * m + 1] * z[round][r].y);
-      }
-      wave_lds_sync();
-      fft256<false>(work[wave][0], work[wave][1], tw, lane);
-      const float2* Z = work[wave][0];
-      const size_t row = (size_t)b * a.Tp + f;
-#pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const int k = lane + 64 * r;
-        if (k > 256) break;
-        float2 Xk;
-        if (k == 256) {
-          Xk = make_float2(Z[0].x - Z[0].y, 0.f);
-        } else {
-          const float2 zk = Z[k], zm = conjf2(Z[(M256 - k) & 255]);
-          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y + zm.y));
-          const float2 Dd = csub(zk, zm);
-          const float2 O = make_float2(0.5f * Dd.y, -0.5f * Dd.x);
-          Xk = cadd(E, cmul(tw[k], O));
-        }
-        if (k == 0) Xk = make_float2(0.f, 0.f);       // DC removed (model/model.py:24,410)
-        const float mag = hypotf(Xk.x, Xk.y);
-        const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
-        if (pass == 0 && own) a.X[row * NBIN + k] = Xk;
-        if (pass == (two ? 1 : 0)) {
-          S[fi][k + 1] = live ? db : 0.f;
-          if (two && own) a.specdb[row * SPEC_LD + k] = db;
-        }
-      }
-      wave_lds_sync();  // this wave's next transform overwrites work[wave]
-    }
-  }
-  lds_sync();
-  // activity gate over the own frames (k_gate's arithmetic, model/model.py:414-419)
-  float w[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) w[i] = a.gate_w[i];
-  const float bias = a.gate_w[9], alpha = a.gate_w[10];
-  float st[2] = {0.f, 0.f};
-  for (int i = tid; i < GATE_ROWS * NBIN; i += 256) {
-    const int ti = i / NBIN, f = i % NBIN;
-    const int t = f0 + ti;
-    const float x = S[ti + 1][f + 1];
-    float y = x;
-    if (a.activity) {
-      float g = bias;
-#pragma unroll
-      for (int di = 0; di < 3; ++di)
-#pragma unroll
-        for (int dj = 0; dj < 3; ++dj) g = fmaf(w[di * 3 + dj], S[ti + dj][f + di], g);
-      y = x * prelu_f(g, alpha);
-    }
-    if (f >= 1) a.S0[((size_t)b * a.Tp + t) * CH + f - 1] = y;
-    if (t < T && f >= 1) { st[0] += y; st[1] += y * y; }
-  }
-  block_reduce_store<2>(st, red, a.gate_rec + ((size_t)b * (a.Tp / GATE_ROWS) + blockIdx.y) * 2);
-}
-
-hipError_t launch_stft_gate(const StftArgs& a, hipStream_t s) {
-  if (a.N <= HOP || a.Tp % GATE_ROWS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_stft_gate, dim3(a.B, a.Tp / GATE_ROWS), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
 // VAD conv1_1 for VAD_ROWS = 32 frames of one (utterance, speaker). Thread = input channel c (the
 // 257th channel is folded in after the lane reduction): the thread's 20 taps stay in registers, its
 // R + 4 input samples (one coalesced 1 KB row read per frame, every load in flight at once) form a
@@ -243,6 +133,13 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   const int bs = blockIdx.x, b = bs >> 1, s = bs & 1;
   const int t0 = blockIdx.y * R;
   const int T = a.T;
+  // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
+  unsigned long long* const pr = a.probe ? a.probe + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+  auto stamp = [&](int k) {
+    if (pr && tid == 0) pr[k] = __builtin_amdgcn_s_memtime();
+  };
+  if (pr && tid == 0) pr[0] = wall_clock64();
+  stamp(1);
   float m[R + 4];
 #pragma unroll
   for (int r = 0; r < R + 4; ++r) m[r] = vad_in(a, b, s, t0 - 2 + r, tid);
@@ -261,6 +158,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
       for (int k = 0; k < 5; ++k) v = fmaf(w[o][k], m[i + k], v);
       acc[4 * i + o] = v;
     }
+  stamp(2);
   // recursive halving over the lanes: partner lane ^ msk; the lower lane keeps the lower half
 #pragma unroll
   for (int msk = 32, n = NV; msk >= 1; msk >>= 1, n >>= 1) {
@@ -282,9 +180,11 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
       acc[1] = fmaf(a.w1[((size_t)(o0 + 1) * NBIN + NBIN - 1) * 5 + k], x, acc[1]);
     }
   }
+  stamp(3);
   part[wave][2 * lane] = acc[0];
   part[wave][2 * lane + 1] = acc[1];
   lds_sync();
+  stamp(4);
   float st[2] = {0.f, 0.f};
   if (tid < NV) {
     const int ii = tid >> 2, o = tid & 3;
@@ -296,6 +196,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   }
   const int nrec = a.Tp / R;
   block_reduce_store<2>(st, red, a.out_rec + ((size_t)bs * nrec + blockIdx.y) * 2);
+  stamp(5);
 }
 
 hipError_t launch_vad1(const Vad1Args& a, hipStream_t s) {

@@ -14,6 +14,7 @@ from conftest import CONFIGS, config_of, load_golden
 pytestmark = pytest.mark.gpu
 
 SEP_TOL = 1e-4
+VAD_PROB_TOL = 1e-3  # VAD probabilities; labels bit-exact (see test_gpu_parity.VAD_PROB_TOL)
 SCHED_TOL = 1e-5
 DEV = "cuda"
 
@@ -50,7 +51,7 @@ def test_fused_matches_reference_goldens(cname, case, nets):
     sep, vad = sep.cpu().numpy(), vad.cpu().numpy()
     assert np.abs(sep - g["sep"]).max() <= SEP_TOL
     assert np.array_equal(vad >= 0.5, g["vad"] >= 0.5)
-    assert np.abs(vad - g["vad"]).max() <= 1e-4
+    assert np.abs(vad - g["vad"]).max() <= VAD_PROB_TOL
 
 
 @pytest.mark.parametrize("cname", CONFIGS)

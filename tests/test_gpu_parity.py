@@ -12,6 +12,11 @@ from conftest import CASES, CONFIGS, config_of, load_golden
 pytestmark = pytest.mark.gpu
 
 SEP_TOL = 1e-4   # north_star: waveform max-abs
+# VAD probabilities (the labels are compared bit-exact): the VAD head sees 10 log10 |X|^2 of near-silent
+# bins, where any float32 FFT's rounding (~1e-7 of max |X|) moves the dB a lot; perturbing the reference
+# STFT by 3e-8 max|X| already moves its own VAD probabilities by up to 6e-4 on the ragged golden
+# (tests/test_oracle_golden.py::test_reference_vad_sensitivity), so 1e-3 is the honest bound.
+VAD_PROB_TOL = 1e-3
 DEV = "cuda"
 
 
@@ -51,7 +56,7 @@ def test_forward_matches_reference(cname, case, models):
     assert err <= SEP_TOL, f"sep max-abs {err}"
     assert vad.shape == g["vad"].shape
     assert np.array_equal(vad >= 0.5, g["vad"] >= 0.5), "VAD labels differ"
-    assert np.abs(vad - g["vad"]).max() <= 1e-4
+    assert np.abs(vad - g["vad"]).max() <= VAD_PROB_TOL
     assert np.abs(net.masks_b.cpu().numpy() - g["masks_b"]).max() <= 2e-3
     assert np.abs(net.spectrum.cpu().numpy() - g["spectrum"]).max() <= 0.2
     mps = torch.sigmoid(torch.from_numpy(g["masks_b"])).reshape(net.mask_per_speaker.shape).numpy()
