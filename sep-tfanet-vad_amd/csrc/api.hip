@@ -976,7 +976,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ha.wscale = h->P(h->wout.scale); ha.bias = h->P(h->bo);
     ha.masks = w.masks;
     if (ev()) return SEPVAD_E_HIP;
+    TailProbe tp(h, s, "head");
+    ha.probe = tp.buf;
     HIPCHK(launch_head(ha, s));
+    HIPCHK(tp.dump(2LL * ha.B * ha.G, 1));
     if (ev()) return SEPVAD_E_HIP;
     if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
     if (out->masks_b) {

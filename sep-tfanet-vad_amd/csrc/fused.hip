@@ -187,11 +187,11 @@ struct WLay {
 // static register ring; the first PD steps are already in (rh, rl) on entry.
 // PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
 // hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
-template <int NS, int LDA, int PRE>
+template <int NS, int LDA, int PRE, int RD = PD>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                          u32x4v (&rh)[PD], u32x4v (&rl)[PD], int lane) {
-  static_assert(NS % PD == 0 && NS > PD, "K steps");
+                                          u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
+  static_assert(NS % RD == 0 && NS > RD, "K steps");
   constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
   // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
@@ -217,8 +217,8 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
                                                     acc, 0, 0, 0);
     }
     if (pf) {
-      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + PD) * 1024, 0);
-      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + PD) * 1024, 0);
+      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
+      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
     }
     ah = nh; al = nl;
     // pipeline shape of a step: next step's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
@@ -230,19 +230,19 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
     __builtin_amdgcn_sched_barrier(0);
   };
 #pragma unroll
-  for (int s0 = 0; s0 < NS - PD; s0 += PD) {
+  for (int s0 = 0; s0 < NS - RD; s0 += RD) {
 #pragma unroll
-    for (int i = 0; i < PD; ++i) step(s0 + i, i, true);
+    for (int i = 0; i < RD; ++i) step(s0 + i, i, true);
   }
 #pragma unroll
-  for (int i = 0; i < PD; ++i) step(NS - PD + i, i, false);
+  for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
 }
 
-template <int PRE>
+template <int PRE, int RD = PD>
 __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                           u32x4v (&rh)[PD], u32x4v (&rl)[PD]) {
+                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD]) {
 #pragma unroll
-  for (int s = 0; s < PD; ++s) {
+  for (int s = 0; s < RD; ++s) {
     rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
     if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
   }
@@ -1005,24 +1005,31 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule. One workgroup per 32-frame slice of
-// an utterance (the k_tcn members' slices), 9 waves x 2 tiles of 32 output channels (576 = 18 tiles): A =
-// GN_out(PReLU(x')) of the slice into LDS once (statistics from k_tcn's per-member records, fixed order),
-// then each wave streams its tiles' weights from L2 in fragment order (wave_gemm) and stores its channels
-// of the masks rows. Replaces the 64x64-tiled head GEMM, which re-read x' for each of its 9 channel tiles.
+// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule. Two workgroups per 32-frame slice of
+// an utterance (the k_tcn members' slices), each 9 waves x one tile of 32 output channels (half of the 18
+// tiles of the 576 = 2 x 257 (+ pad) channels): A = GN_out(PReLU(x')) of the slice into LDS (statistics from
+// k_tcn's per-member records, fixed order), then each wave streams its tile's weights from L2 in fragment
+// order (wave_gemm) and stores its channels of the masks rows. Two resident workgroups per CU (<= 96 VGPRs)
+// overlap one's prologue with the other's weight stream (a CU streams 590 KB of fp16x3 weights per slice
+// either way).
 constexpr int HTHR = 576;
 template <int PRE>
-__global__ __launch_bounds__(HTHR) void k_head(HeadArgs a) {
+__global__ __launch_bounds__(HTHR, 5) void k_head(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 Ahi[FR * LDX];
   __shared__ __attribute__((aligned(16))) _Float16 Alo[PRE == PREC_F16X3 ? FR * LDX : 8];
   __shared__ float hs[2][CH];
   __shared__ double dred[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int u = blockIdx.x / a.G, g = blockIdx.x % a.G, t0 = g * FR;
-  // first tile's weight ring in flight with the x' loads and the statistics
-  const __amdgpu_buffer_rsrc_t wh = rsrc_of(a.wh), wl = rsrc_of(PRE == PREC_F16X3 ? a.wl : a.wh);
-  u32x4v rh[PD], rl[PD];
-  prefetch_w<PRE>(wh, wl, (wave * NS1 * 64 + lane) * 16, rh, rl);
+  const int sl = blockIdx.x >> 1, q = blockIdx.x & 1;  // slice, half of the channel tiles
+  const int u = sl / a.G, g = sl % a.G, t0 = g * FR;
+  const int j = wave + 9 * q;  // this wave's tile: channels [32 j, 32 j + 32)
+  // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
+  unsigned long long* const pr = a.probe ? a.probe + (size_t)blockIdx.x * 8 : nullptr;
+  auto stamp = [&](int k) {
+    if (pr && tid == 0) pr[k] = __builtin_amdgcn_s_memtime();
+  };
+  if (pr && tid == 0) pr[0] = wall_clock64();
+  stamp(1);
   // raw x' of the slice: 32 rows x 256 channels, thread-contiguous channels (coalesced 1 KB rows)
   constexpr int NV = FR * CH / HTHR + 1;  // 15
   float xv[NV];
@@ -1037,6 +1044,7 @@ __global__ __launch_bounds__(HTHR) void k_head(HeadArgs a) {
     dred[tid] = s;
   }
   __syncthreads();
+  stamp(2);
   if (tid < CH) {
     float mu, rs;
     gn_moments_f(dred[0], dred[1], a.inv_ch, 1e-5f, mu, rs);
@@ -1055,29 +1063,32 @@ __global__ __launch_bounds__(HTHR) void k_head(HeadArgs a) {
     }
   }
   __syncthreads();
-  // two tiles per wave: channels [32 j, 32 j + 32), j = wave, wave + 9; the second tile's ring is
-  // issued before the first tile's stores
+  stamp(3);
+  // the tile's weight ring (issued here, not in the prologue: the register budget of 5 waves per SIMD;
+  // the co-resident workgroup's GEMM covers this one's prologue)
+  const __amdgpu_buffer_rsrc_t wh = rsrc_of(a.wh), wl = rsrc_of(PRE == PREC_F16X3 ? a.wl : a.wh);
+  const int voff = (j * NS1 * 64 + lane) * 16;
+  constexpr int HRD = 4;  // ring depth (k_tcn uses PD = 8 at 2 waves per SIMD)
+  u32x4v rh[HRD], rl[HRD];
+  prefetch_w<PRE, HRD>(wh, wl, voff, rh, rl);
   const int hl4 = 4 * (lane >> 5);
-  f32x16v acc[2];
+  f32x16v acc;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int j = wave + 9 * q;
-    const int voff = (j * NS1 * 64 + lane) * 16;
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  wave_gemm<NS1, LDX, PRE, HRD>(acc, Ahi, Alo, wh, wl, voff, rh, rl, lane);
+  stamp(4);
+  const int m = 32 * j + (lane & 31);
+  const float ws = a.wscale[m], bias = a.bias[m];
+  float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + m;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
-    wave_gemm<NS1, LDX, PRE>(acc[q], Ahi, Alo, wh, wl, voff, rh, rl, lane);
-    if (q == 0) prefetch_w<PRE>(wh, wl, ((j + 9) * NS1 * 64 + lane) * 16, rh, rl);
-    const int m = 32 * j + (lane & 31);
-    const float ws = a.wscale[m], bias = a.bias[m];
-    float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + m;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = fmaf(acc[q][r], ws, bias);
-  }
+  for (int r = 0; r < 16; ++r) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = fmaf(acc[r], ws, bias);
+  stamp(5);
 }
 
 hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   if (a.G < 1 || a.G * FR > a.Tp) return hipErrorInvalidValue;
-  const dim3 grid(a.B * a.G);
+  static_assert(2 * 9 * 32 == MOUT_PAD, "two workgroups x 9 waves x 32 channels cover the head's padded rows");
+  const dim3 grid(2 * a.B * a.G);
   switch (a.prec) {
     case PREC_F16X3: hipLaunchKernelGGL(k_head<PREC_F16X3>, grid, dim3(HTHR), 0, s, a); break;
     case PREC_F16: hipLaunchKernelGGL(k_head<PREC_F16>, grid, dim3(HTHR), 0, s, a); break;

@@ -309,6 +309,7 @@ struct HeadArgs {
   const __half* wh; const __half* wl;  // fragment-ordered W planes [MOUT_PAD/32][CH/16][64][8] (wl: F16X3 only)
   const float* wscale; const float* bias;  // [MOUT_PAD]
   float* masks;          // [B][Tp][MOUT_PAD]
+  unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_head(const HeadArgs& a, hipStream_t s);
 int tcn_blocks_per_cu(int ln_mode, int prec);

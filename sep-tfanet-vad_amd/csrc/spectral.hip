@@ -9,6 +9,8 @@
 //
 // FFT: a 512-point real transform = one 256-point complex transform of z[m] = x[2m] + i x[2m+1]
 // (radix-4 Stockham, 4 stages, one wave per transform in LDS) plus the split/merge twiddle step.
+#include <type_traits>
+
 #include "device_common.h"
 #include "fft_common.h"
 
@@ -159,17 +161,43 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
       acc[4 * i + o] = v;
     }
   stamp(2);
-  // recursive halving over the lanes: partner lane ^ msk; the lower lane keeps the lower half
+  // recursive halving over the lanes: a lane whose bit msk is clear keeps the lower half of its outputs,
+  // its partner (bit set, same higher bits) the upper half. Bits 32 / 16: one v_permlane32/16_swap per pair
+  // (the swap hands each lane its partner's item of the kept half: kept = own + swapped, no selects);
+  // bits 8, 4: DPP row_mirror / row_half_mirror partners (lane i <-> 15 - i / 7 - i: opposite bit, same
+  // higher bits), bits 2, 1: DPP quad_perm xor. Same index mapping as an xor butterfly (lane L ends with
+  // outputs 2L, 2L+1); cdna_hip_programming.md T12/T21.
+  // (inline asm: with this hipcc the __builtin_amdgcn_permlane{16,32}_swap pair result came back as the
+  // same register twice, x + x, tools/probe_src/halving.hip; "s_nop 1" covers the VALU-write -> permlane
+  // hazard, cdna_hip_programming.md T21)
 #pragma unroll
-  for (int msk = 32, n = NV; msk >= 1; msk >>= 1, n >>= 1) {
+  for (int j = 0; j < NV / 2; ++j) {
+    float x = acc[j], y = acc[j + NV / 2];
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+    acc[j] = x + y;
+  }
+#pragma unroll
+  for (int j = 0; j < NV / 4; ++j) {
+    float x = acc[j], y = acc[j + NV / 4];
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+    acc[j] = x + y;
+  }
+  auto dpp_level = [&](auto CTRL, int msk, int n) {
+    constexpr int C = decltype(CTRL)::value;
     const bool hi = (lane & msk) != 0;
 #pragma unroll
-    for (int j = 0; j < n / 2; ++j) {
-      const float send = hi ? acc[j] : acc[j + n / 2];
-      const float keep = hi ? acc[j + n / 2] : acc[j];
-      acc[j] = keep + __shfl_xor(send, msk);
+    for (int j = 0; j < NV / 8; ++j) {
+      if (j < n / 2) {
+        const float send = hi ? acc[j] : acc[j + n / 2];
+        const float keep = hi ? acc[j + n / 2] : acc[j];
+        acc[j] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), C, 0xf, 0xf, false));
+      }
     }
-  }
+  };
+  dpp_level(std::integral_constant<int, 0x140>{}, 8, NV / 4);  // row_mirror
+  dpp_level(std::integral_constant<int, 0x141>{}, 4, NV / 8);  // row_half_mirror
+  dpp_level(std::integral_constant<int, 0x4e>{}, 2, NV / 16);  // quad_perm [2,3,0,1]
+  dpp_level(std::integral_constant<int, 0xb1>{}, 1, NV / 32);  // quad_perm [1,0,3,2]
   // channel 256 (the Nyquist bin): lane L of wave 0 adds its contribution to outputs 2L, 2L+1
   if (wave == 0) {
     const int i = lane >> 1, o0 = 2 * (lane & 1);
