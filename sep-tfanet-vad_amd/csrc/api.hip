@@ -66,6 +66,7 @@ struct Workspace {
   size_t bytes = 0;
   float2* X; float* specdb; float* S0; float* O[2]; float* A; float* R;
   float* masks; float* colsum; float* rowsum; float* at; float* af; float* vy; float* vad;
+  float* vP;  // [B][2][Tp][HEAD_VAD_N] VAD conv1_1 tap products from k_head (fused schedule)
   __half* Dhi; __half* Dlo; float* D32;  // res_out operand d (fp16 split planes, or fp32, same bytes)
   // partial records of the statistics producers (deterministic per-workgroup sums)
   double* rec_gate; double* rec_g1; double* rec_dw; double* rec_mom; double* rec_hs; double* rec_vad;
@@ -82,6 +83,7 @@ Workspace ws_view(const Workspace& w, int b0, int Tp) {
   v.Dhi = w.Dhi + u * HID; v.Dlo = w.Dlo + u * HID; v.D32 = w.D32 + u * HID;
   v.colsum = w.colsum + u * (CH / TILE); v.rowsum = w.rowsum + (size_t)b0 * (Tp / TILE) * CH;
   v.at = w.at + u; v.af = w.af + (size_t)b0 * CH; v.vy = w.vy + u * 2 * 4; v.vad = w.vad + u * 2;
+  v.vP = w.vP + u * 2 * HEAD_VAD_N;
   v.rec_gate = w.rec_gate + (size_t)b0 * (Tp / GATE_ROWS) * 2;
   v.rec_g1 = w.rec_g1 + (size_t)b0 * (Tp / TILE) * (CH / TILE) * 2;
   v.rec_dw = w.rec_dw + (size_t)b0 * (Tp / STAT_ROWS) * 2;
@@ -122,6 +124,12 @@ struct sepvad_model {
   size_t ln_g = 0, ln_b = 0;
   PackedW wout;
   size_t out_g = 0, out_b = 0, bo = 0;
+  // k_head's copy of the output head: speaker q's 257 rows at rows [288 q, 288 q + 257) (zero rows to 288), so a
+  // workgroup of 9 x 32 rows is one speaker; and the VAD conv1_1 as that workgroup's second GEMM (HEAD_VAD:
+  // B[c][4 k + o] = w1[o][c][k], 20 of 32 columns, 288 speaker-local channels)
+  PackedW wout_spk, vadw;
+  size_t bo_spk = 0;
+  float vad_sx = 1.f;  // fp16 range scale of the VAD GEMM's A operand (undone by vadw.scale)
   float out_a = 0.f;
   size_t v_w1 = 0, v_b1 = 0, v_g = 0, v_b = 0, v_w2 = 0;
   float v_a = 0.f, v_b2 = 0.f;
@@ -315,6 +323,7 @@ int ws_reserve(StreamCtx* c, int B, int N) {
   const size_t oRg = take(bt / GATE_ROWS * 16 + 16), oR1 = take((size_t)Bm * (CH / TILE) * (Tm / TILE) * 16);
   const size_t oRd = take(bt / STAT_ROWS * 16 + 16), oRm = take(bt / STAT_ROWS * NMOM * 8 + 16);
   const size_t oRh = take(bt / STAT_ROWS * 16 + 16), oRv = take(bt * 2 / VAD_ROWS * 16 + 16);
+  const size_t oVp = take(bt * 2 * HEAD_VAD_N * 4);
   char* base = nullptr;
   HIPCHK(hipMalloc(&base, off));
   HIPCHK(hipMemset(base, 0, off));
@@ -327,6 +336,7 @@ int ws_reserve(StreamCtx* c, int B, int N) {
   w.af = (float*)(base + oAf); w.vy = (float*)(base + oVy); w.vad = (float*)(base + oV);
   w.rec_gate = (double*)(base + oRg); w.rec_g1 = (double*)(base + oR1); w.rec_dw = (double*)(base + oRd);
   w.rec_mom = (double*)(base + oRm); w.rec_hs = (double*)(base + oRh); w.rec_vad = (double*)(base + oRv);
+  w.vP = (float*)(base + oVp);
   return SEPVAD_OK;
 }
 
@@ -679,10 +689,19 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     h->out_b = pk.add(ob, CH);
     const int eh = range_exp(gn_bound(og, ob, CH));  // head A operand = GN_out(PReLU(x'))
     h->out_sx = std::ldexp(1.f, -eh);
-    h->wout = pack_pointwise(pk, fold_wn(gg, vv, MOUT, CH), MOUT, CH, MOUT_PAD, eh);
+    const std::vector<float> wo = fold_wn(gg, vv, MOUT, CH);
+    h->wout = pack_pointwise(pk, wo, MOUT, CH, MOUT_PAD, eh);
     std::vector<float> bpad(MOUT_PAD, 0.f);
     std::memcpy(bpad.data(), bb, MOUT * sizeof(float));
     h->bo = pk.add(bpad);
+    std::vector<float> ws((size_t)MOUT_PAD * CH, 0.f), bs(MOUT_PAD, 0.f);
+    for (int q = 0; q < 2; ++q)
+      for (int i = 0; i < NBIN; ++i) {
+        std::memcpy(&ws[((size_t)q * HEAD_SPK + i) * CH], &wo[((size_t)q * NBIN + i) * CH], CH * sizeof(float));
+        bs[q * HEAD_SPK + i] = bb[q * NBIN + i];
+      }
+    h->wout_spk = pack_pointwise(pk, ws, MOUT_PAD, CH, MOUT_PAD, eh);
+    h->bo_spk = pk.add(bs);
   }
   // VAD head (model/model.py:153-171)
   if (c.final_vad) {
@@ -696,7 +715,29 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const float* v2 = get("vad.output_layer_vad.weight_v", 12);
     const float* b2 = get("vad.output_layer_vad.bias", 1);
     BAIL();
-    h->v_w1 = pk.add(fold_wn(g1, v1, 4, NBIN * 5));
+    const std::vector<float> w1 = fold_wn(g1, v1, 4, NBIN * 5);  // [o][c][k]
+    h->v_w1 = pk.add(w1);
+    std::vector<float> wv((size_t)32 * HEAD_SPK, 0.f);  // [4 k + o][speaker-local channel c]
+    for (int o = 0; o < 4; ++o)
+      for (int c2 = 0; c2 < NBIN; ++c2)
+        for (int k = 0; k < 5; ++k) wv[(size_t)(4 * k + o) * HEAD_SPK + c2] = w1[((size_t)o * NBIN + c2) * 5 + k];
+    // range guard of the VAD GEMM's A operand (the masks tile, fp16 split): |masks| <= max over rows of
+    // sum_c |W| * bound(GN_out(..)) + |bias|; the tile is scaled by 2^-e on its way into the split and the
+    // columns' scale carries 2^e back
+    double mb = 0.0;
+    {
+      const std::vector<float> wo = fold_wn(get("TCN.output.2.weight_g", MOUT), get("TCN.output.2.weight_v", (int64_t)MOUT * CH), MOUT, CH);
+      const float* ob2 = get("TCN.output.2.bias", MOUT);
+      const double ab = gn_bound(get("TCN.output.1.weight", CH), get("TCN.output.1.bias", CH), CH);
+      for (int r = 0; r < MOUT; ++r) {
+        double sr = 0.0;
+        for (int i = 0; i < CH; ++i) sr += std::fabs((double)wo[(size_t)r * CH + i]);
+        mb = std::max(mb, sr * ab + std::fabs((double)ob2[r]));
+      }
+    }
+    const int ev_ = range_exp(mb);
+    h->vad_sx = std::ldexp(1.f, -ev_);
+    h->vadw = pack_pointwise(pk, wv, HEAD_VAD_N, HEAD_SPK, 32, ev_);
     h->v_b1 = pk.add(b1, 4);
     h->v_a = a[0];
     h->v_g = pk.add(gg, 4);
@@ -886,6 +927,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   const int G = (T + FR - 1) / FR;
   const bool use_fused = fused_ok(h, T);
   h->last_fused = use_fused;
+  const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
+  // the VAD conv1_1 as k_head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
+  const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
     // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
     TcnArgs ta{};
@@ -971,10 +1015,15 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ha.Xfin = w.O[0]; ha.rec = w.rec_hs;
     ha.g = h->P(h->out_g); ha.be = h->P(h->out_b); ha.alpha = h->out_a; ha.sx = h->out_sx;
     ha.inv_ch = 1.0 / ((double)CH * T);
-    ha.wh = h->H(h->prec == PREC_BF16 ? h->wout.fbf : h->wout.fhi);
-    ha.wl = h->H(h->wout.flo);
-    ha.wscale = h->P(h->wout.scale); ha.bias = h->P(h->bo);
+    ha.wh = h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
+    ha.wl = h->H(h->wout_spk.flo);
+    ha.wscale = h->P(h->wout_spk.scale); ha.bias = h->P(h->bo_spk);
     ha.masks = w.masks;
+    if (vad_in_head) {
+      ha.vP = w.vP;
+      ha.vwh = h->H(h->vadw.fhi); ha.vwl = h->H(h->vadw.flo); ha.vwscale = h->P(h->vadw.scale);
+      ha.vsx = h->vad_sx;
+    }
     if (ev()) return SEPVAD_E_HIP;
     TailProbe tp(h, s, "head");
     ha.probe = tp.buf;
@@ -1074,10 +1123,18 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
     }
   }
-  // 5. VAD conv1_1 (model/model.py:424-427,434-436)
-  const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
+  // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from k_head's tap products (k_vad_feat,
+  // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
-  if (has_vad) {
+  if (vad_in_head) {
+    VadFeatArgs vf{};
+    vf.B = B; vf.T = T; vf.Tp = Tp; vf.vP = w.vP;
+    vf.b1 = h->P(h->v_b1); vf.alpha = h->v_a;
+    vf.g = h->P(h->v_g); vf.be = h->P(h->v_b); vf.eps = 1e-8f;
+    vf.feat = w.vy;
+    HIPCHK(launch_vad_feat(vf, s));
+  }
+  if (has_vad && !vad_in_head) {
     Vad1Args v{};
     v.B = B; v.T = T; v.Tp = Tp; v.masked_speakers = c.final_vad_masked_speakers;
     v.masks = w.masks; v.X = w.X;
@@ -1101,6 +1158,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       is.ret_smooth = kw_on && kw->return_smoothed_vad;
       is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
       is.vy = w.vy; is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
+      is.vy_norm = vad_in_head;
       is.vgn = gn_src(w.rec_vad, Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
       is.vad_out = out->vad ? out->vad + u2 * T : w.vad;
     }

@@ -22,6 +22,13 @@ __device__ __forceinline__ void lds_sync() {
   asm volatile("" ::: "memory");
 }
 
+// Orders this wave's LDS writes before its later LDS reads (for buffers that belong to one wave: no
+// workgroup barrier needed).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Sum over the 64 lanes of a wave; callers use lane 0's value (fixed order => deterministic).
 template <typename Tv>
 __device__ __forceinline__ Tv wave_sum(Tv v) {

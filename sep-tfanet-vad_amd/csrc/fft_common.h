@@ -52,12 +52,6 @@ __device__ __forceinline__ void fft_stage(const float2* in, float2* out, const f
   out[idxD + 3 * Ns] = csub(a1, a3);
 }
 
-// Orders this wave's LDS writes before its later LDS reads (the buffers of a transform belong to one
-// wave: no workgroup barrier is needed between its stages).
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
 
 // 256-point transform of one wave ping-ponging between its buffers b0 and b1 (4 stages: result back
 // in b0); the caller's buffers must be complete for this wave (wave_lds_sync or a barrier) on entry.

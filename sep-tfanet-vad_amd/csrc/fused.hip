@@ -1005,24 +1005,34 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule. Two workgroups per 32-frame slice of
-// an utterance (the k_tcn members' slices), each 9 waves x one tile of 32 output channels (half of the 18
-// tiles of the 576 = 2 x 257 (+ pad) channels): A = GN_out(PReLU(x')) of the slice into LDS (statistics from
-// k_tcn's per-member records, fixed order), then each wave streams its tile's weights from L2 in fragment
-// order (wave_gemm) and stores its channels of the masks rows. Two resident workgroups per CU (<= 96 VGPRs)
-// overlap one's prologue with the other's weight stream (a CU streams 590 KB of fp16x3 weights per slice
-// either way).
+// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule, with the VAD head's conv1_1
+// (model/model.py:158-160) as a second GEMM on the masks tile. Two workgroups per 32-frame slice of an
+// utterance (the k_tcn members' slices), one per speaker: 9 waves x one tile of 32 of the speaker's 288 rows
+// (257 + zero rows; the per-speaker weight copy wout_spk). A = GN_out(PReLU(x')) of the slice into LDS once
+// (statistics from k_tcn's per-member records, fixed order), each wave streams its tile's weights from L2 in
+// fragment order (wave_gemm) and stores its channels of the masks rows. VAD (a.vP): each wave transposes
+// its 32 x 32 masks tile through LDS into the A operand of P_w = tile . Wv (Wv[c][4k+o] = w1[o][c][k],
+// fp16x3 on v_mfma_f32_32x32x16_f16), the 9 partial P are summed in wave order and stored per frame (20
+// tap products); k_vad_feat finishes the conv (shifted tap sums + bias + PReLU) and BN_1. Together they
+// replace k_vad1 and its 18 MB re-read of the masks.
 constexpr int HTHR = 576;
+constexpr int HVLD = 33;  // row stride (floats) of a wave's masks / P tile in LDS
 template <int PRE>
-__global__ __launch_bounds__(HTHR, 5) void k_head(HeadArgs a) {
-  __shared__ __attribute__((aligned(16))) _Float16 Ahi[FR * LDX];
-  __shared__ __attribute__((aligned(16))) _Float16 Alo[PRE == PREC_F16X3 ? FR * LDX : 8];
+__global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
+  // LDS <= 64 KB (two workgroups per CU: measured, one per CU above that): the VAD tiles of waves 0..7 reuse
+  // the A operand's bytes once every wave's GEMM is done
+  constexpr int AB = 2 * FR * LDX;  // halves: Ahi then Alo
+  static_assert(8 * FR * HVLD * 4 <= AB * 2, "8 VAD tiles fit the A operand's bytes");
+  __shared__ __attribute__((aligned(16))) _Float16 ab[AB];
+  __shared__ __attribute__((aligned(16))) float vt8[FR * HVLD];  // wave 8's VAD tile
   __shared__ float hs[2][CH];
   __shared__ double dred[2];
+  _Float16* const Ahi = ab;
+  _Float16* const Alo = ab + FR * LDX;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sl = blockIdx.x >> 1, q = blockIdx.x & 1;  // slice, half of the channel tiles
+  const int sl = blockIdx.x >> 1, q = blockIdx.x & 1;  // slice, speaker
   const int u = sl / a.G, g = sl % a.G, t0 = g * FR;
-  const int j = wave + 9 * q;  // this wave's tile: channels [32 j, 32 j + 32)
+  const int j = 9 * q + wave;  // this wave's row tile of wout_spk: speaker-local rows [32 wave, 32 wave + 32)
   // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
   unsigned long long* const pr = a.probe ? a.probe + (size_t)blockIdx.x * 8 : nullptr;
   auto stamp = [&](int k) {
@@ -1039,8 +1049,13 @@ __global__ __launch_bounds__(HTHR, 5) void k_head(HeadArgs a) {
     xv[k] = i < FR * CH ? a.Xfin[((size_t)u * a.Tp + t0) * CH + i] : 0.f;
   }
   if (tid < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in order
+    double v[FG_MAX];
+#pragma unroll
+    for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < a.G ? a.rec[((size_t)u * a.G + mm) * 2 + tid] : 0.0;
     double s = 0.0;
-    for (int mm = 0; mm < a.G; ++mm) s += a.rec[((size_t)u * a.G + mm) * 2 + tid];
+#pragma unroll
+    for (int mm = 0; mm < FG_MAX; ++mm)
+      if (mm < a.G) s += v[mm];
     dred[tid] = s;
   }
   __syncthreads();
@@ -1077,17 +1092,74 @@ __global__ __launch_bounds__(HTHR, 5) void k_head(HeadArgs a) {
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   wave_gemm<NS1, LDX, PRE, HRD>(acc, Ahi, Alo, wh, wl, voff, rh, rl, lane);
   stamp(4);
-  const int m = 32 * j + (lane & 31);
-  const float ws = a.wscale[m], bias = a.bias[m];
-  float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + m;
+  // the VAD GEMM's B fragments (this wave's two K steps, hi and lo), in flight during the mask stores
+  f16x8 vb[2][2];
+  if (a.vP != nullptr) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = fmaf(acc[r], ws, bias);
+    for (int st = 0; st < 2; ++st) {
+      vb[st][0] = *reinterpret_cast<const f16x8*>(a.vwh + ((size_t)(2 * wave + st) * 64 + lane) * 8);
+      vb[st][1] = *reinterpret_cast<const f16x8*>(a.vwl + ((size_t)(2 * wave + st) * 64 + lane) * 8);
+    }
+  }
+  const int c = 32 * wave + (lane & 31);  // speaker-local channel (rows >= 257 are zero rows)
+  const float ws = a.wscale[32 * j + (lane & 31)], bias = a.bias[32 * j + (lane & 31)];
+  float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + q * NBIN + c;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc[r] = fmaf(acc[r], ws, bias);
+    if (c < NBIN) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = acc[r];
+  }
+  if (a.vP == nullptr) {
+    stamp(5);
+    return;
+  }
+  float* const vtb = reinterpret_cast<float*>(ab);
+  auto vtile = [&](int w) { return w < 8 ? vtb + w * FR * HVLD : vt8; };
+  float* tile = vtile(wave);
+  __syncthreads();  // every wave's GEMM has read A: its bytes become the VAD tiles
+#pragma unroll
+  for (int r = 0; r < 16; ++r)  // (range guard of the VAD GEMM's fp16 split)
+    tile[((r & 3) + 8 * (r >> 2) + hl4) * HVLD + (lane & 31)] = acc[r] * a.vsx;
+  // ---- VAD conv1_1 tap products of this wave's 32 channels: P_w[t][n] = sum_c tile[t][c] Wv[c][n] ----
+  wave_lds_sync();
+  f32x16v pv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pv[r] = 0.f;
+  {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {  // K = 32 channels = 2 steps of 16
+      const float* ar = tile + (lane & 31) * HVLD + 16 * st + 8 * (lane >> 5);
+      f16x8 ah, al;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = ar[e];
+        const _Float16 h = (_Float16)x;
+        ah[e] = h;
+        al[e] = (_Float16)(x - (float)h);
+      }
+      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, vb[st][0], pv, 0, 0, 0);
+      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][1], pv, 0, 0, 0);
+      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][0], pv, 0, 0, 0);
+    }
+  }
+  wave_lds_sync();  // every lane's tile reads done before the partial P overwrites the tile
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tile[((r & 3) + 8 * (r >> 2) + hl4) * HVLD + (lane & 31)] = pv[r];
+  __syncthreads();
+  float* vp = a.vP + (((size_t)u * 2 + q) * a.Tp + t0) * HEAD_VAD_N;
+  for (int i = tid; i < FR * HEAD_VAD_N; i += HTHR) {
+    const int t = i / HEAD_VAD_N, n = i - t * HEAD_VAD_N;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) sum += vtile(w)[t * HVLD + n];  // wave (channel) order
+    vp[i] = t0 + t < a.T ? sum * a.vwscale[n] : 0.f;  // conv zero padding outside [0, T)
+  }
   stamp(5);
 }
 
 hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   if (a.G < 1 || a.G * FR > a.Tp) return hipErrorInvalidValue;
-  static_assert(2 * 9 * 32 == MOUT_PAD, "two workgroups x 9 waves x 32 channels cover the head's padded rows");
+  static_assert(2 * 9 * 32 == MOUT_PAD && HEAD_SPK == 9 * 32, "one workgroup of 9 x 32 rows per speaker");
   const dim3 grid(2 * a.B * a.G);
   switch (a.prec) {
     case PREC_F16X3: hipLaunchKernelGGL(k_head<PREC_F16X3>, grid, dim3(HTHR), 0, s, a); break;

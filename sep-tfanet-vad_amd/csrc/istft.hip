@@ -159,20 +159,22 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   if (vad) {
     float g = 0.f, be = 0.f;
     if (tid < 8) { g = a.vgn.g[tid & 3]; be = a.vgn.be[tid & 3]; }
-    reduce_records(rec_src(a.vgn, 2 * b, 2), rec_src(a.vgn, 2 * b + 1, 2), dacc);  // BN_1 = GroupNorm(1, 4)
-    lds_sync();
-    if (tid < 8) {
-      const int sp = tid >> 2, o = tid & 3;
-      float mu, rs;
-      gn_moments(dacc[2 * sp], dacc[2 * sp + 1], 4.0 * T, a.vgn.eps, mu, rs);
-      vs[sp][o] = rs * g;
-      vh[sp][o] = be - vs[sp][o] * mu;
+    if (!a.vy_norm) {  // BN_1 = GroupNorm(1, 4) from k_vad1's records (else vy arrives normalised)
+      reduce_records(rec_src(a.vgn, 2 * b, 2), rec_src(a.vgn, 2 * b + 1, 2), dacc);
+      lds_sync();
+      if (tid < 8) {
+        const int sp = tid >> 2, o = tid & 3;
+        float mu, rs;
+        gn_moments(dacc[2 * sp], dacc[2 * sp + 1], 4.0 * T, a.vgn.eps, mu, rs);
+        vs[sp][o] = rs * g;
+        vh[sp][o] = be - vs[sp][o] * mu;
+      }
+      lds_sync();
     }
-    lds_sync();
     if (tid < 2 * 4 * NQ) {
       const int sp = tid / (4 * NQ), o = (tid / NQ) % 4, qq = tid % NQ;
       const int f = fbeg - 3 + qq;
-      yn[sp][o][qq] = (f >= 0 && f < T) ? fmaf(yv, vs[sp][o], vh[sp][o]) : 0.f;
+      yn[sp][o][qq] = (f >= 0 && f < T) ? (a.vy_norm ? yv : fmaf(yv, vs[sp][o], vh[sp][o])) : 0.f;
     }
     lds_sync();
     if (tid < 2 * (IP_FR + 4)) {

@@ -21,6 +21,8 @@ constexpr int HID = 512;    // H_dim (depthwise multiplier 2)
 constexpr int TILE = 64;    // GEMM tile edge; Tp is a multiple of TILE
 constexpr int MOUT = 2 * NBIN;  // 514 output-head rows (2 speakers x 257 bins)
 constexpr int MOUT_PAD = 576;   // padded to a multiple of 64 (also the row stride of `masks`)
+constexpr int HEAD_SPK = MOUT_PAD / 2;  // k_head's per-speaker row block (257 rows + zero rows)
+constexpr int HEAD_VAD_N = 20;          // VAD conv1_1 tap products per frame: 5 taps x 4 outputs
 constexpr int SPEC_LD = 260;    // row stride of the frame-major dB spectrum
 constexpr int STAT_ROWS = 8;    // rows (frames) per workgroup of the stats kernels
 constexpr int PROBE_SLOTS = 16;  // per-workgroup timestamps of a probed GEMM launch
@@ -174,6 +176,15 @@ struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4)
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 
+struct VadFeatArgs {     // k_vad_feat: conv1_1 finish + BN_1 from k_head's tap products
+  int B, T, Tp;
+  const float* vP;       // [B][2][Tp][HEAD_VAD_N]
+  const float* b1; float alpha;       // conv1_1 bias [4], relu_1 PReLU
+  const float* g; const float* be; float eps;  // BN_1 affine, eps
+  float* feat;           // [B][2][4][Tp] normalised features (the k_istft VAD tail's input)
+};
+hipError_t launch_vad_feat(const VadFeatArgs& a, hipStream_t s);
+
 struct IstftArgs {
   int BS, S, N, T, Tp, est_mode;  // est_mode 1: forward (mask X, VAD); 0: est given (debug entry)
   const float2* X;       // [B][Tp][NBIN]
@@ -184,7 +195,8 @@ struct IstftArgs {
   // VAD tail (model/model.py:160-179,444-457); has_vad = 0 -> no VAD, gain 1
   int has_vad, kw_enabled, filt, ret_smooth;
   float thr;
-  const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output
+  const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output (k_vad1), or BN_1-normalised (vy_norm)
+  int vy_norm;           // vy already normalised (k_vad_feat): no BN_1 records
   GnSrc vgn;             // BN_1 = GroupNorm(1, 4) over [4, T] per (utterance, speaker); rec [B*S][..]
   const float* w2; float b2;          // output_layer_vad [4][3], bias
   float* vad_out;        // [B][S][T]
@@ -309,6 +321,11 @@ struct HeadArgs {
   const __half* wh; const __half* wl;  // fragment-ordered W planes [MOUT_PAD/32][CH/16][64][8] (wl: F16X3 only)
   const float* wscale; const float* bias;  // [MOUT_PAD]
   float* masks;          // [B][Tp][MOUT_PAD]
+  // VAD conv1_1 as a second GEMM on the masks tile (nullable vP: off): vP[b][s][t][4 k + o] =
+  // sum_c masks[t][s 257 + c] w1[o][c][k], zero for t >= T; B planes in fragment order, per-column scale
+  const __half* vwh; const __half* vwl; const float* vwscale;
+  float vsx;             // range scale of the masks tile as the VAD GEMM's A operand (undone by vwscale)
+  float* vP;             // [B][2][Tp][HEAD_VAD_N]
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_head(const HeadArgs& a, hipStream_t s);

@@ -227,6 +227,53 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   stamp(5);
 }
 
+// k_vad_feat: the VAD head's conv1_1 finished from k_head's tap products (fused schedule), one workgroup per
+// (utterance, speaker): y[t][o] = sum_k P[t - 2 + k][4 k + o] (zero outside [0, T)), v = PReLU(y + b1),
+// BN_1 = GroupNorm(1, 4) over [4, T] (block sums in double, wave order), feat = v * s[o] + h[o] for
+// k_istft_pair's VAD tail (model/model.py:158-176).
+__global__ __launch_bounds__(256) void k_vad_feat(VadFeatArgs a) {
+  __shared__ float red[2 * 16];
+  __shared__ double dacc[2];
+  __shared__ float vs[4], vh[4];
+  const int tid = threadIdx.x, bs = blockIdx.x, T = a.T;
+  const float* P = a.vP + (size_t)bs * a.Tp * HEAD_VAD_N;
+  constexpr int NI = 4;  // 4 x T <= 1024 items = 4 per thread
+  static_assert(4 * 256 <= NI * 256, "items per thread (T <= 256)");
+  float v[NI], st[2] = {0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const int i = tid + 256 * it, t = i >> 2, o = i & 3;
+    float y = 0.f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int tt = t - 2 + k;
+      y += (i < 4 * T && tt >= 0 && tt < T) ? P[(size_t)tt * HEAD_VAD_N + 4 * k + o] : 0.f;
+    }
+    v[it] = prelu_f(y + a.b1[o], a.alpha);
+    if (i < 4 * T) { st[0] += v[it]; st[1] += v[it] * v[it]; }
+  }
+  block_reduce_store<2>(st, red, dacc);
+  lds_sync();
+  if (tid < 4) {
+    float mu, rs;
+    gn_moments(dacc[0], dacc[1], 4.0 * T, a.eps, mu, rs);
+    vs[tid] = rs * a.g[tid];
+    vh[tid] = a.be[tid] - vs[tid] * mu;
+  }
+  lds_sync();
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const int i = tid + 256 * it, t = i >> 2, o = i & 3;
+    if (i < 4 * T) a.feat[((size_t)bs * 4 + o) * a.Tp + t] = fmaf(v[it], vs[o], vh[o]);
+  }
+}
+
+hipError_t launch_vad_feat(const VadFeatArgs& a, hipStream_t s) {
+  if (a.T < 1 || a.T > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_vad_feat, dim3(a.B * 2), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_vad1(const Vad1Args& a, hipStream_t s) {
   if (a.Tp % VAD_ROWS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_vad1, dim3(a.B * 2, a.Tp / VAD_ROWS), dim3(256), 0, s, a);

@@ -3,7 +3,10 @@ reference goldens and the multi-kernel schedule, over every group size it suppor
 1..8 workgroups per utterance), batches larger than one resident wave of groups, and the fallback.
 
 Tolerances: separated waveforms max-abs <= 1e-4 vs the reference/oracle (north_star); the two
-schedules differ only in the order of fp32 partial sums, so they agree to 1e-5.
+schedules differ only in the order of fp32 partial sums, so the waveforms agree to 1e-5. The VAD
+probabilities agree to 1e-4: the fused schedule computes the VAD conv1_1 as k_head's second GEMM (fp16x3
+MFMA, channel sums in MFMA order), the other with k_vad1 (VALU, lane-tree order), and the VAD head
+amplifies rounding (tests/test_oracle_golden.py::test_reference_vad_sensitivity).
 """
 import numpy as np
 import pytest
@@ -16,6 +19,7 @@ pytestmark = pytest.mark.gpu
 SEP_TOL = 1e-4
 VAD_PROB_TOL = 1e-3  # VAD probabilities; labels bit-exact (see test_gpu_parity.VAD_PROB_TOL)
 SCHED_TOL = 1e-5
+VAD_SCHED_TOL = 1e-4
 DEV = "cuda"
 
 
@@ -68,7 +72,7 @@ def test_fused_vs_multikernel_and_oracle(cname, N, nets, state_dicts):
     sm, vm, em, used_m = _run(net, x.to(DEV), False)
     assert not used_m
     assert (sf - sm).abs().max().item() <= SCHED_TOL
-    assert (vf - vm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
     assert (ef - em).abs().max().item() <= 1e-3
     om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
     s_ref, v_ref, _ = om(x[:1])
