@@ -54,6 +54,9 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_MOM5
 #define TCN_MOM5 1   // recursive-LN moment record from 5 per-thread row sums, channel weights applied once
 #endif
+#ifndef HEAD_VT_ALIAS
+#define HEAD_VT_ALIAS 1  // k_head's VAD tiles alias the A operand (40 KB LDS, one more barrier) or own LDS (74 KB)
+#endif
 #ifndef TCN_PFX
 #define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
 #endif
@@ -1019,16 +1022,23 @@ constexpr int HTHR = 576;
 constexpr int HVLD = 33;  // row stride (floats) of a wave's masks / P tile in LDS
 template <int PRE>
 __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
-  // LDS <= 64 KB (two workgroups per CU: measured, one per CU above that): the VAD tiles of waves 0..7 reuse
-  // the A operand's bytes once every wave's GEMM is done
+#if HEAD_VT_ALIAS
+  // the VAD tiles of waves 0..7 reuse the A operand's bytes once every wave's GEMM is done (40 KB of LDS)
   constexpr int AB = 2 * FR * LDX;  // halves: Ahi then Alo
   static_assert(8 * FR * HVLD * 4 <= AB * 2, "8 VAD tiles fit the A operand's bytes");
   __shared__ __attribute__((aligned(16))) _Float16 ab[AB];
   __shared__ __attribute__((aligned(16))) float vt8[FR * HVLD];  // wave 8's VAD tile
-  __shared__ float hs[2][CH];
-  __shared__ double dred[2];
   _Float16* const Ahi = ab;
   _Float16* const Alo = ab + FR * LDX;
+#else
+  // own VAD tiles, no barrier before them: 74 KB of LDS, and then only one workgroup per CU is resident
+  // (measured, r02aq: 21.6 vs 19.1 us)
+  __shared__ __attribute__((aligned(16))) _Float16 Ahi[FR * LDX];
+  __shared__ __attribute__((aligned(16))) _Float16 Alo[PRE == PREC_F16X3 ? FR * LDX : 8];
+  __shared__ __attribute__((aligned(16))) float vts[9][FR * HVLD];
+#endif
+  __shared__ float hs[2][CH];
+  __shared__ double dred[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int sl = blockIdx.x >> 1, q = blockIdx.x & 1;  // slice, speaker
   const int u = sl / a.G, g = sl % a.G, t0 = g * FR;
@@ -1113,10 +1123,14 @@ __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
     stamp(5);
     return;
   }
+#if HEAD_VT_ALIAS
   float* const vtb = reinterpret_cast<float*>(ab);
   auto vtile = [&](int w) { return w < 8 ? vtb + w * FR * HVLD : vt8; };
-  float* tile = vtile(wave);
   __syncthreads();  // every wave's GEMM has read A: its bytes become the VAD tiles
+#else
+  auto vtile = [&](int w) { return vts[w]; };
+#endif
+  float* tile = vtile(wave);
 #pragma unroll
   for (int r = 0; r < 16; ++r)  // (range guard of the VAD GEMM's fp16 split)
     tile[((r & 3) + 8 * (r >> 2) + hl4) * HVLD + (lane & 31)] = acc[r] * a.vsx;
