@@ -1,7 +1,7 @@
 // The whole TCN separator (24 x [DepthConv1d + TF_Attention + recursive/residual LN], reference
 // model/model.py:103-149,182-208,271-357) as ONE persistent launch: k_tcn.
 //
-// Work split: an utterance of T frames is owned by a GROUP of G = ceil(T/32) workgroups; member g owns
+// Work split: an utterance of T frames is owned by a GROUP of G = ceil(T/32) <= 32 workgroups; member g owns
 // frames [32g, 32g+32) and ALL 256 channels of them, for every block. Inside a block every 1x1 conv is a
 // row-local GEMM (frames x channels) and the depthwise conv needs `dil` halo frames, so the only
 // cross-workgroup traffic of a block is four small hand-offs inside the group:
@@ -635,10 +635,14 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         for (int k = 0; k < 4; ++k)
           if (hrow[k] >= 0) sm.H[hrow[k] * CH + hcol[k]] = p[k] != nullptr ? __builtin_bit_cast(float, v[k]) : 0.f;
 #if TCN_GNW
-        if (wave_s == NTHR / 64 - 1) {  // the GN1 pollers' wave: moments before the barrier
-          float mu, rs;
-          member_moments_w(v[4], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
-          if (lane == 0) { sm.gmom[0] = mu; sm.gmom[1] = rs; }
+        if (G <= FG_WAVE) {
+          if (wave_s == NTHR / 64 - 1) {  // the GN1 pollers' wave: moments before the barrier
+            float mu, rs;
+            member_moments_w(v[4], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
+            if (lane == 0) { sm.gmom[0] = mu; sm.gmom[1] = rs; }
+          }
+        } else if (sk >= 0) {  // long utterances: the words span two waves, finished from LDS below
+          sm.gw[sk] = v[4];
         }
 #else
         if (sk >= 0) sm.gw[sk] = v[4];
@@ -657,7 +661,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float sc, sh;
         {
 #if TCN_GNW
-          const float mu = sm.gmom[0], rs = sm.gmom[1];
+          float mu, rs;
+          if (G <= FG_WAVE) {
+            mu = sm.gmom[0]; rs = sm.gmom[1];
+          } else {  // same doubles in the same member order as member_moments_w
+            const double2 acc = member_sums2(sm.gw, G, lane);
+            gn_moments_f(acc.x, acc.y, a.inv_ch, 1e-8f, mu, rs);
+          }
 #else
           const double2 acc = member_sums2(sm.gw, G, lane);
           float mu, rs;
@@ -739,10 +749,14 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         unsigned v[1];
         gpoll<1>(p, tag2, v, a);
 #if TCN_GNW
-        if (wave_s == 0) {  // the GN2 pollers' wave: moments before the barrier (eps rescaled with d)
-          float mu, rs;
-          member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
-          if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
+        if (G <= FG_WAVE) {
+          if (wave_s == 0) {  // the GN2 pollers' wave: moments before the barrier (eps rescaled with d)
+            float mu, rs;
+            member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
+            if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
+          }
+        } else if (tid < 4 * G) {
+          sm.gw[tid] = v[0];
         }
 #else
         if (tid < 4 * G) sm.gw[tid] = v[0];
@@ -756,7 +770,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float fmu, frs;
         {
 #if TCN_GNW
-          fmu = sm.gmom[2]; frs = sm.gmom[3];
+          if (G <= FG_WAVE) {
+            fmu = sm.gmom[2]; frs = sm.gmom[3];
+          } else {
+            const double2 acc = member_sums2(sm.gw, G, lane);
+            gn_moments_f(acc.x, acc.y, a.inv_hid, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
+          }
 #else
           const double2 acc = member_sums2(sm.gw, G, lane);  // every member's GN2 sums, member order
 #if TCN_FMOM
@@ -801,26 +820,37 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(7);
         // consume P3: rowsums of every member (a_f), channel sums of the 4 frames either side (a_t)
         {
-          const u64* pp[FG_MAX];
-          unsigned v[FG_MAX];
-#pragma unroll
-          for (int mm = 0; mm < FG_MAX; ++mm) pp[mm] = (tid < CH && mm < G) ? slot(mm, e3) + GW_ROW + tid : nullptr;
+          const u64* pp[FG_CHUNK];
+          unsigned v[FG_CHUNK];
           int mi = -1;  // a_t input index (frame t0 - 4 + mi) served by this thread
+          const u64* pat = nullptr;
           if (tid >= CH && tid < CH + 8) {
             const int k = tid - CH;
             mi = k < 4 ? k : FR + k;             // 0..3 and 36..39
             const int tl = mi - 4, t = t0 + tl;
-            if (t >= 0 && t < T) pp[0] = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
+            if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
           }
-          gpoll<FG_MAX>(pp, tag3, v, a);
+          // FG_CHUNK members per pass (one pass up to 8 members), summed in member order
+          float s = 0.f, vat = 0.f;
+          for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
+#pragma unroll
+            for (int mm = 0; mm < FG_CHUNK; ++mm)
+              pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
+            if (c0 == 0 && mi >= 0) pp[0] = pat;
+            gpoll<FG_CHUNK>(pp, tag3, v, a);
+            if (tid < CH) {
+#pragma unroll
+              for (int mm = 0; mm < FG_CHUNK; ++mm)
+                if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
+            }
+            if (c0 == 0 && pat != nullptr) vat = __builtin_bit_cast(float, v[0]);
+          }
           __syncthreads();  // csum complete (read below by other threads)
           if (tid < CH) {
-            float s = 0.f;
-            for (int mm = 0; mm < G; ++mm) s += __builtin_bit_cast(float, v[mm]);
             sm.vec[tid + 4] = s / (float)T;
             if (tid < 4) { sm.vec[tid] = 0.f; sm.vec[CH + 4 + tid] = 0.f; sm.yf[tid] = 0.f; sm.yf[CH + 4 + tid] = 0.f; }
           } else if (mi >= 0) {
-            sm.mC[mi] = pp[0] != nullptr ? __builtin_bit_cast(float, v[0]) / (float)CH : 0.f;
+            sm.mC[mi] = vat / (float)CH;
           } else if (tid >= CH + 8 && tid < CH + 8 + FR) {
             const int tl = tid - CH - 8;
             sm.mC[tl + 4] = (t0 + tl < T) ? sm.csum[tl] / (float)CH : 0.f;
@@ -926,6 +956,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           unsigned v[1];
           gpoll<1>(pp, tag4, v, a);
           if (k < 2 * NMOM * G) sm.gw[k] = v[0];
+          if (2 * NMOM * G > NTHR) {  // more than 23 members: the remaining words in a second pass
+            const int k2 = tid + NTHR;
+            const u64* p2[1] = {k2 < 2 * NMOM * G ? slot(k2 / (2 * NMOM), e4) + GW_STAT + k2 % (2 * NMOM) : nullptr};
+            gpoll<1>(p2, tag4, v, a);
+            if (k2 < 2 * NMOM * G) sm.gw[k2] = v[0];
+          }
         }
       TPROBE(11);
         __syncthreads();  // every member's moment words in LDS
@@ -1059,13 +1095,15 @@ __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
     xv[k] = i < FR * CH ? a.Xfin[((size_t)u * a.Tp + t0) * CH + i] : 0.f;
   }
   if (tid < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in order
-    double v[FG_MAX];
-#pragma unroll
-    for (int mm = 0; mm < FG_MAX; ++mm) v[mm] = mm < a.G ? a.rec[((size_t)u * a.G + mm) * 2 + tid] : 0.0;
     double s = 0.0;
+    for (int c0 = 0; c0 < a.G; c0 += FG_CHUNK) {
+      double v[FG_CHUNK];
 #pragma unroll
-    for (int mm = 0; mm < FG_MAX; ++mm)
-      if (mm < a.G) s += v[mm];
+      for (int mm = 0; mm < FG_CHUNK; ++mm) v[mm] = c0 + mm < a.G ? a.rec[((size_t)u * a.G + c0 + mm) * 2 + tid] : 0.0;
+#pragma unroll
+      for (int mm = 0; mm < FG_CHUNK; ++mm)
+        if (c0 + mm < a.G) s += v[mm];
+    }
     dred[tid] = s;
   }
   __syncthreads();

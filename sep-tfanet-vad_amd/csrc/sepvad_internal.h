@@ -266,7 +266,9 @@ hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
 // ---- fused persistent TCN (fused.hip) ----
 constexpr int FR = 32;          // frames per workgroup
-constexpr int FG_MAX = 8;       // workgroups per utterance (T <= 256)
+constexpr int FG_MAX = 32;      // workgroups per utterance (T <= 1024: 16.4 s at 16 kHz in one fused forward)
+constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
+constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
 constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
 constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
