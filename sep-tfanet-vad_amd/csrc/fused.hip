@@ -60,6 +60,14 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_PFX
 #define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
 #endif
+#ifndef TCN_EARLY
+#define TCN_EARLY 0  // bit 0: next block's conv1d weight ring issued with the res_out epilogue rows (else the x' update
+                     // rows); bit 1: the res_out weight ring with the conv1d epilogue rows (else the dwconv rows)
+#endif
+#ifndef TCN_MED3
+#define TCN_MED3 0   // PReLU as med3(x, a x, +-inf) (prelu_m): off — it stops hipcc's SLP packing of the dwconv
+                     // (static VALU 3798 -> 4403) and measured within noise (profiles/r02ar_ab_early.txt)
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -77,7 +85,10 @@ constexpr int NTHR = 512;         // 8 waves; wave w owns output channels [32w, 
 constexpr int LDX = CH + 8;       // x' row stride (halves): 132 dwords == 4 (mod 64) => conflict-free b128 reads
 constexpr int LDD = HID + 8;      // d row stride (halves): 260 dwords == 4 (mod 64)
 constexpr int HROW = FR + 8;      // conv1d output rows incl. 4 halo rows on each side
-constexpr int PD = 8;             // weight K steps in flight per wave
+#ifndef TCN_PD
+#define TCN_PD 8
+#endif
+constexpr int PD = TCN_PD;        // weight K steps in flight per wave
 constexpr int NS1 = CH / 16;      // conv1d K steps (256 / 16)
 constexpr int NS2 = HID / 16;     // res_out K steps (512 / 16)
 
@@ -98,6 +109,14 @@ struct TcnSmem {
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
+
+// PReLU x > 0 ? x : a x (torch) as one v_med3 of x, a x and a bound chosen once per slope: for a <= 1 it is
+// max(x, a x) (bound +inf), for a > 1 min(x, a x) (bound -inf). Returns one of the two operands (the same value
+// as prelu_f for every finite x; the surrounding code generation, and so the rounding of later sums, differs).
+__device__ __forceinline__ float prelu_bound(float a) { return a <= 1.f ? __builtin_inff() : -__builtin_inff(); }
+__device__ __forceinline__ float prelu_m(float x, float a, float bound) {
+  return __builtin_amdgcn_fmed3f(x, a * x, bound);
+}
 
 // Wave-uniform copies (readfirstlane) of values loaded from the block-parameter table: the compiler cannot
 // prove those loads uniform, and a buffer descriptor in VGPRs becomes a waterfall loop per access.
@@ -194,7 +213,7 @@ template <int NS, int LDA, int PRE, int RD = PD>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
-  static_assert(NS % RD == 0 && NS > RD, "K steps");
+  static_assert(NS % RD == 0 && NS >= RD, "K steps");
   constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
   // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
@@ -589,10 +608,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         u64* s1 = slot(g, e1);
         float st[2] = {0.f, 0.f};
+        const float pb1 = prelu_bound(a1);
+        const __amdgpu_buffer_rsrc_t w2he = rsrc_of(wb + WL::W2H), w2le = rsrc_of(wb + WL::W2L);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+          if ((TCN_EARLY & 2) && r % 2 == 0) prefetch_w1<PRE>(w2he, w2le, voff2, rh, rl, r / 2);
           const int tl = trow(r);
-          float v = prelu_f(fmaf(acc[r], ws, bias), a1);
+          float v = TCN_MED3 ? prelu_m(fmaf(acc[r], ws, bias), a1, pb1) : prelu_f(fmaf(acc[r], ws, bias), a1);
           v = (t0 + tl < T) ? v : 0.f;
           sm.H[(tl + 4) * CH + m] = v;
           st[0] += v; st[1] += v * v;
@@ -649,13 +671,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        if (!TCN_PFX) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
+        if (!TCN_PFX && !(TCN_EARLY & 2)) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
         const int c = tid & (CH - 1), rh0 = (tid >> 8) * (FR / 2);
-        const float a2 = pm[PB_A2];
+        const float a2 = pm[PB_A2], pb2 = prelu_bound(a2);
         // GN1 affine of this thread's channel, computed in-thread from the members' sums (member order,
         // as gn_affine: no LDS round trip, no barrier)
         float sc, sh;
@@ -707,7 +729,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
-            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
+            if (TCN_PFX && !(TCN_EARLY & 2) && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -717,7 +739,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               x = fmaf(wv[q][0], hv[i], x);
               x = fmaf(wv[q][1], hv[i + D], x);
               x = fmaf(wv[q][2], hv[i + 2 * D], x);
-              const float v = prelu_f(x, a2) * vo;
+              const float v = (TCN_MED3 ? prelu_m(x, a2, pb2) : prelu_f(x, a2)) * vo;
               st[0] += v; st[1] += v * v;
               dv[q] = v;
             }
@@ -766,6 +788,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       f32x16v& rv = acc;  // r = res_out output, in place
       const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
+      // next block's conv1d weights (the last block re-reads its own weights: the loads stay unconditional
+      // and in bounds)
+      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
+      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
       {
         float fmu, frs;
         {
@@ -792,6 +818,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = trow(r);
           rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
           const float rm = t0 + tl < T ? rv[r] : 0.f;
+          if ((TCN_EARLY & 1) && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
           rsum += rm;
           csr[r] = half_total(rm);  // this frame's sum over the wave's 32 channels (lanes 31 / 63)
         }
@@ -1000,18 +1027,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
       if (TCN_SUB == 0) TPROBE(13);
       }
-      // next block's conv1d weights: in flight during the x' update
-      // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
-      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
-      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
-      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
+      // next block's conv1d weights: in flight during the x' update (TCN_EARLY: since the res_out epilogue)
+      if (!TCN_PFX && !(TCN_EARLY & 1) && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
+          if (TCN_PFX && !(TCN_EARLY & 1) && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
