@@ -1,7 +1,7 @@
 """Throughput of the MI355X Sep-TFAnet^VAD forward path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f16x3|fp32|bf16|f16]
-                    [--workload offline|cfg4|cfg5|stream]
+                    [--workload offline|cfg4|cfg5|long|stream]
 
 One step = one ``SeparationModel.forward`` (config_with_vad.json) over a resident batch of 64
 synthetic 2-speaker mixtures of 32 000 samples (4 s @ 8 kHz resampled to 16 kHz by the
@@ -249,10 +249,11 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32", "bf16", "f16"],
                     help="GEMM arithmetic: f16x3 / fp32 meet the fp32 parity gates (default f16x3); bf16 / f16 are "
                          "the reduced-precision arms (BASELINE cfg 2 / cfg 5; tolerance in DESIGN.md §4)")
-    ap.add_argument("--workload", default="offline", choices=["offline", "cfg4", "cfg5", "stream"],
+    ap.add_argument("--workload", default="offline", choices=["offline", "cfg4", "cfg5", "long", "stream"],
                     help="offline: cfg 2 (default, the BASELINE metric: B=64, N=32000); cfg4: 8 s reverberant "
                          "mixtures, B=64/GPU, N=64000 (T=251); cfg5: B=128/GPU, N=32000 (run with --precision "
-                         "f16 for the fp16 arm); stream: cfg 3 streaming wrapper")
+                         "f16 for the fp16 arm); long: 16 s files as only_inference.py forwards them (B=8/GPU, "
+                         "N=256000, T=1001: fused groups of 32 workgroups); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
     rc = launch_ranks(args)
     if rc is not None:
@@ -276,7 +277,8 @@ def main():
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     net = net.eval().to(dev)
     net.native_precision = args.precision
-    B0, N0 = {"offline": (B_PER_GPU, N_SAMPLES), "cfg4": (64, 64000), "cfg5": (128, 32000)}[args.workload]
+    B0, N0 = {"offline": (B_PER_GPU, N_SAMPLES), "cfg4": (64, 64000), "cfg5": (128, 32000),
+              "long": (8, 256000)}[args.workload]
     B = args.batch or B0
     N = args.samples or N0
     T = 1 + N // 256
@@ -373,7 +375,9 @@ def main():
                              "cfg4": f"cfg4 config_with_vad.json forward on image-method reverberant mixtures, "
                                      f"B={B}/GPU, N={N} samples (8 s @ 8 kHz), T={T} frames",
                              "cfg5": f"cfg5 config_with_vad.json forward, B={B}/GPU, N={N} samples, T={T} "
-                                     f"frames, {args.precision} GEMMs"}[args.workload]
+                                     f"frames, {args.precision} GEMMs",
+                             "long": f"long files (only_inference.py:90-91 forwards a whole file), config_with_vad.json, "
+                                     f"B={B}/GPU, N={N} samples (16 s @ 16 kHz), T={T} frames"}[args.workload]
                             + "; full forward: STFT, 24 TCN blocks, VAD, iSTFT, est (side attributes on read)",
                 "global_batch": world * B,
                 "seq_len": N,
