@@ -9,6 +9,24 @@
 
 namespace sepvad {
 
+// Stores of the large inter-kernel buffers (X, S0, x', masks, est, sep): with SEPVAD_NT non-temporal, so the
+// lines do not sit dirty in the XCD's L2 until the kernel boundary writes them back (A/B switch).
+#ifndef SEPVAD_NT
+#define SEPVAD_NT 0
+#endif
+__device__ __forceinline__ void st_out(float* p, float v) {
+  if constexpr (SEPVAD_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void st_out(float2* p, float2 v) {
+  if constexpr (SEPVAD_NT) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 __device__ __forceinline__ float prelu_f(float x, float w) { return x > 0.f ? x : w * x; }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 

@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = t0 + trow(r);
-        if (t < Tp) Xu[trow(r) * CH + mt_] = o[r];
+        if (t < Tp) st_out(Xu + trow(r) * CH + mt_, o[r]);
         if (t < T) {
           const float pv = prelu_f(o[r], a.alpha_h);
           st[0] += pv; st[1] += pv * pv;
@@ -1179,7 +1179,7 @@ __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     acc[r] = fmaf(acc[r], ws, bias);
-    if (c < NBIN) out[(size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD] = acc[r];
+    if (c < NBIN) st_out(out + (size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD, acc[r]);
   }
   if (a.vP == nullptr) {
     stamp(5);

@@ -228,9 +228,9 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
         if (a.est_out) {
           const float2 e = spec[sp][fo + 1][k];
           const float gg = gain[sp][fo + 1];
-          a.est_out[o] = make_float2(gg * e.x, gg * e.y);
+          st_out(a.est_out + o, make_float2(gg * e.x, gg * e.y));
         }
-        if (a.mask_out) a.mask_out[o] = sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]);
+        if (a.mask_out) st_out(a.mask_out + o, sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]));
       }
     }
     lds_sync();  // the transforms below overwrite the rows
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
       float num = 0.f;
       if (j < T) num += reinterpret_cast<const float*>(spec[sp][j - fbeg])[q];  // frame j, first half
       num += reinterpret_cast<const float*>(spec[sp][j - 1 - fbeg])[q + HOP];    // frame j-1, second half
-      yb[n] = num * (j < T ? inv_mid : inv_last);
+      st_out(yb + n, num * (j < T ? inv_mid : inv_last));
     }
   }
   stamp(5);

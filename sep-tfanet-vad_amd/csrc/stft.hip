@@ -108,7 +108,7 @@ __global__ __launch_bounds__(SG_THREADS) void k_stft_gate(StftArgs a) {
         if (k == 0) Xk = make_float2(0.f, 0.f);  // DC removed (model/model.py:24,410)
         const float mag = hypotf(Xk.x, Xk.y);     // torch.abs(complex)
         const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
-        if (store_x && own) a.X[xrow * NBIN + k] = Xk;
+        if (store_x && own) st_out(a.X + xrow * NBIN + k, Xk);
         if (store_db) {
           S[fi][k + 1] = live ? db : 0.f;
           if (two && own) a.specdb[xrow * SPEC_LD + k] = db;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(SG_THREADS) void k_stft_gate(StftArgs a) {
           for (int dj = 0; dj < 3; ++dj) g = fmaf(w[di * 3 + dj], col[di][r + dj], g);
         y = x * prelu_f(g, alpha);
       }
-      s0p[(size_t)r * CH] = y;
+      st_out(s0p + (size_t)r * CH, y);
       if (f0 + r0 + r < T) { s1 += y; s2 += y * y; }
     }
     st[0] = h == 0 ? s1 : 0.f;
