@@ -68,6 +68,14 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #define TCN_MED3 0   // PReLU as med3(x, a x, +-inf) (prelu_m): off — it stops hipcc's SLP packing of the dwconv
                      // (static VALU 3798 -> 4403) and measured within noise (profiles/r02ar_ab_early.txt)
 #endif
+#ifndef TCN_COLW
+#define TCN_COLW 0   // P3 frame sums: the 8 boundary frames' per-wave partials published from registers before the
+                     // barrier (consumers add the 8 wave partials in wave order: the same bits as the summed word);
+                     // bitwise equal, but measured 17 us per forward slower (profiles/r02au_ab_colw.txt): off
+#endif
+#ifndef TCN_SLEEP
+#define TCN_SLEEP 1  // s_sleep argument between poll passes (units of 64 clocks)
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -179,7 +187,7 @@ __device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, un
       }
     }
     if (ok) return;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(TCN_SLEEP);
     if ((++spins & 255u) == 0 &&
         (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
       giveup(a);
@@ -192,7 +200,7 @@ constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq h
 constexpr int GW_TOP = 4;           // P1: rows 0..dil-1      [dil][256]
 constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
 constexpr int GW_ROW = 0;           // P3: per-channel sums over own frames [256]
-constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
+constexpr int GW_COL = CH;          // P3: per-frame channel sums [32] (TCN_COLW: boundary frames' wave partials [8][8])
 static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
@@ -826,6 +834,19 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if ((lane & 31) == 31) {  // one branch for the 16 frame sums
 #pragma unroll
             for (int r = 0; r < 16; ++r) sm.cs[trow(r)][wave] = csr[r];
+#if TCN_COLW
+            // P3 words: the per-wave partial channel sums of the frames the neighbours read (a_t), straight from
+            // registers: lane 31 holds frames 0..3 (r = 0..3), lane 63 frames 28..31 (r = 12..15); word
+            // GW_COL + 8 * idx + wave, idx = frame (0..3) or 4 + frame - 28
+            u64* const sc = slot(g, e3) + GW_COL + wave;
+            if (hl == 0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) gputf(sc + 8 * r, tag3, csr[r], l2);
+            } else {
+#pragma unroll
+              for (int r = 12; r < 16; ++r) gputf(sc + 8 * (r - 8), tag3, csr[r], l2);
+            }
+#endif
           }
           // P3 words: per-channel sums over own frames (a_f)
           rsum += __shfl_xor(rsum, 32);
@@ -835,6 +856,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // ---- TF_Attention (model/model.py:182-208) ----
       if (TCN_SUB == 3) TPROBE(13);
       if (tf) {
+#if !TCN_COLW
         __syncthreads();
         if (TCN_SUB == 3) TPROBE(14);
         if (tid < FR) {  // P3 words: per-frame channel sums (a_t)
@@ -844,6 +866,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sm.csum[tid] = s;
           gputf(slot(g, e3) + GW_COL + tid, tag3, s, l2);
         }
+#endif
       TPROBE(7);
         // consume P3: rowsums of every member (a_f), channel sums of the 4 frames either side (a_t)
         {
@@ -855,7 +878,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             const int k = tid - CH;
             mi = k < 4 ? k : FR + k;             // 0..3 and 36..39
             const int tl = mi - 4, t = t0 + tl;
+#if TCN_COLW
+            static_assert(FG_CHUNK == NTHR / 64, "one poll slot per wave partial");
+            if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + 8 * (tl + 8) : slot(g + 1, e3) + GW_COL + 8 * (tl - FR);
+#else
             if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
+#endif
           }
           // FG_CHUNK members per pass (one pass up to 8 members), summed in member order
           float s = 0.f, vat = 0.f;
@@ -863,14 +891,28 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
             for (int mm = 0; mm < FG_CHUNK; ++mm)
               pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
+#if TCN_COLW
+            if (c0 == 0 && mi >= 0) {
+#pragma unroll
+              for (int w = 0; w < FG_CHUNK; ++w) pp[w] = pat != nullptr ? pat + w : nullptr;
+            }
+#else
             if (c0 == 0 && mi >= 0) pp[0] = pat;
+#endif
             gpoll<FG_CHUNK>(pp, tag3, v, a);
             if (tid < CH) {
 #pragma unroll
               for (int mm = 0; mm < FG_CHUNK; ++mm)
                 if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
+#if TCN_COLW
+            if (c0 == 0 && pat != nullptr) {  // the 8 wave partials in wave order (as the producer's csum)
+#pragma unroll
+              for (int w = 0; w < FG_CHUNK; ++w) vat += __builtin_bit_cast(float, v[w]);
+            }
+#else
             if (c0 == 0 && pat != nullptr) vat = __builtin_bit_cast(float, v[0]);
+#endif
           }
           __syncthreads();  // csum complete (read below by other threads)
           if (tid < CH) {
@@ -880,7 +922,14 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             sm.mC[mi] = vat / (float)CH;
           } else if (tid >= CH + 8 && tid < CH + 8 + FR) {
             const int tl = tid - CH - 8;
+#if TCN_COLW
+            float cs = 0.f;
+#pragma unroll
+            for (int sl = 0; sl < 8; ++sl) cs += sm.cs[tl][sl];
+            sm.mC[tl + 4] = (t0 + tl < T) ? cs / (float)CH : 0.f;
+#else
             sm.mC[tl + 4] = (t0 + tl < T) ? sm.csum[tl] / (float)CH : 0.f;
+#endif
           }
         }
         __syncthreads();
