@@ -1126,7 +1126,11 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from k_head's tap products (k_vad_feat,
   // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
-  if (vad_in_head) {
+  // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, the same arithmetic; measured
+  // equal speed: 114.2k vs 114.4k utt/s, profiles/r02av_ab_vadfeat.txt — the in-kernel BN_1 sums lengthen
+  // k_istft_pair by what the launch saves), default 1: k_vad_feat
+  const bool vad_taps_in_istft = vad_in_head && !env_int("SEPVAD_VAD_FEAT", 1);
+  if (vad_in_head && !vad_taps_in_istft) {
     VadFeatArgs vf{};
     vf.B = B; vf.T = T; vf.Tp = Tp; vf.vP = w.vP;
     vf.b1 = h->P(h->v_b1); vf.alpha = h->v_a;
@@ -1158,7 +1162,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       is.ret_smooth = kw_on && kw->return_smoothed_vad;
       is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
       is.vy = w.vy; is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
-      is.vy_norm = vad_in_head;
+      is.vy_norm = vad_in_head && !vad_taps_in_istft;
+      if (vad_taps_in_istft) {
+        is.vP = w.vP; is.vb1 = h->P(h->v_b1); is.valpha = h->v_a; is.vy = nullptr;
+      }
       is.vgn = gn_src(w.rec_vad, Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
       is.vad_out = out->vad ? out->vad + u2 * T : w.vad;
     }

@@ -100,6 +100,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   __shared__ float gain[2][IP_FR];
   __shared__ float vs[2][4], vh[2][4];
   __shared__ double dacc[4];
+  __shared__ float vred[2 * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x, f0 = blockIdx.y * IP_OWN;
   const int T = a.T;
@@ -129,11 +130,39 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
     mr[1][j] = a.masks[row * MOUT_PAD + NBIN + k];
   }
   constexpr int NQ = IP_FR + 6;
+  // VAD conv1_1 from k_head's tap products (vP mode, model/model.py:158-160): y[t][o] = sum_k P[t-2+k][4k+o]
+  // (zero outside [0, T)), v = PReLU(y + b1[o]) — k_vad_feat's arithmetic, expression for expression
+  const bool taps = vad && a.vP != nullptr;
+  auto tap_v = [&](const float* P, int i, int t, int o) {
+    float y = 0.f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int tt = t - 2 + k;
+      y += (i < 4 * T && tt >= 0 && tt < T) ? P[(size_t)tt * HEAD_VAD_N + 4 * k + o] : 0.f;
+    }
+    return prelu_f(y + a.vb1[o], a.valpha);
+  };
   float yv = 0.f;
   if (vad && tid < 2 * 4 * NQ) {  // thread -> (speaker, feature o, frame q)
     const int sp = tid / (4 * NQ), o = (tid / NQ) % 4, q = tid % NQ;
     const int fc = min(max(fbeg - 3 + q, 0), T - 1);
-    yv = a.vy[(((size_t)b * 2 + sp) * 4 + o) * a.Tp + fc];
+    yv = taps ? tap_v(a.vP + ((size_t)b * 2 + sp) * a.Tp * HEAD_VAD_N, 4 * fc + o, fc, o)
+              : a.vy[(((size_t)b * 2 + sp) * 4 + o) * a.Tp + fc];
+  }
+  if (taps) {  // BN_1 sums of the whole utterance: 256 threads per speaker, k_vad_feat's items and order
+    const int sp = tid >> 8, t8 = tid & 255;
+    const float* P = a.vP + ((size_t)b * 2 + sp) * a.Tp * HEAD_VAD_N;
+    float st[2] = {0.f, 0.f};
+    for (int it = 0; 256 * it < 4 * T; ++it) {
+      const int i = t8 + 256 * it;
+      const float v = tap_v(P, i, i >> 2, i & 3);
+      if (i < 4 * T) { st[0] += v; st[1] += v * v; }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // as block_reduce_store<2> over each speaker's four waves
+      const float ws = wave_sum(st[j]);
+      if (lane == 0) vred[j * 16 + wave] = ws;
+    }
   }
 
   // 1) X sigmoid(mask) of both speakers into the rows (frame-major, coalesced over bins); the VAD gain is
@@ -159,8 +188,18 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   if (vad) {
     float g = 0.f, be = 0.f;
     if (tid < 8) { g = a.vgn.g[tid & 3]; be = a.vgn.be[tid & 3]; }
-    if (!a.vy_norm) {  // BN_1 = GroupNorm(1, 4) from k_vad1's records (else vy arrives normalised)
-      reduce_records(rec_src(a.vgn, 2 * b, 2), rec_src(a.vgn, 2 * b + 1, 2), dacc);
+    if (!a.vy_norm) {  // BN_1 = GroupNorm(1, 4) from k_vad1's records or the tap sums (else vy arrives normalised)
+      if (taps) {
+        lds_sync();  // vred complete
+        if (tid < 4) {  // dacc[2 sp + j]: speaker sp's four wave totals in wave order (double)
+          const int sp = tid >> 1, j = tid & 1;
+          double s = 0.0;
+          for (int i = 0; i < 4; ++i) s += vred[j * 16 + 4 * sp + i];
+          dacc[tid] = s;
+        }
+      } else {
+        reduce_records(rec_src(a.vgn, 2 * b, 2), rec_src(a.vgn, 2 * b + 1, 2), dacc);
+      }
       lds_sync();
       if (tid < 8) {
         const int sp = tid >> 2, o = tid & 3;

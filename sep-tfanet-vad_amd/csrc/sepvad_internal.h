@@ -197,6 +197,9 @@ struct IstftArgs {
   float thr;
   const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output (k_vad1), or BN_1-normalised (vy_norm)
   int vy_norm;           // vy already normalised (k_vad_feat): no BN_1 records
+  const float* vP;       // nullable: k_head's conv1_1 tap products [B][2][Tp][HEAD_VAD_N]; the workgroup finishes
+                         // conv1_1 + PReLU + BN_1 itself (k_vad_feat's arithmetic, no vy / records)
+  const float* vb1; float valpha;     // conv1_1 bias [4], relu_1 PReLU (vP mode)
   GnSrc vgn;             // BN_1 = GroupNorm(1, 4) over [4, T] per (utterance, speaker); rec [B*S][..]
   const float* w2; float b2;          // output_layer_vad [4][3], bias
   float* vad_out;        // [B][S][T]
