@@ -143,3 +143,27 @@ def test_handoff_protocols_bitwise_identical(nets):
         del os.environ["SEPVAD_TCN_XMODE"]
     assert used
     assert torch.equal(a, b) and torch.equal(va, vb)
+
+
+def test_vad_taps_finished_in_istft(nets):
+    """SEPVAD_VAD_FEAT=0: k_istft_pair finishes the VAD conv1_1 + BN_1 from k_head's tap products itself
+    (k_vad_feat's arithmetic); same results as the k_vad_feat schedule up to fp32 rounding, reference-pinned."""
+    import os
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    g = load_golden("with_vad", "cfg")
+    x = torch.from_numpy(synth.make_batch(7, 100000, 515)[0]).to(DEV)
+    a, va, ea, _ = _run(net, x, True)
+    os.environ["SEPVAD_VAD_FEAT"] = "0"
+    try:
+        b, vb, eb, used = _run(net, x, True)
+        sg, vg, _, _ = _run(net, torch.from_numpy(g["x"]).to(DEV), True)
+    finally:
+        del os.environ["SEPVAD_VAD_FEAT"]
+    assert used
+    assert (a - b).abs().max().item() <= 1e-6
+    assert (va - vb).abs().max().item() <= 1e-5
+    assert torch.equal(va >= 0.5, vb >= 0.5)
+    assert np.abs(sg.cpu().numpy() - g["sep"]).max() <= SEP_TOL
+    assert np.array_equal(vg.cpu().numpy() >= 0.5, g["vad"] >= 0.5)
+    assert np.abs(vg.cpu().numpy() - g["vad"]).max() <= VAD_PROB_TOL
