@@ -75,7 +75,7 @@ def res_out_bytes(B, T):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r02ak_pmc_tcn.json"      # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r02aw_pmc_tcn.json"      # fused schedule (k_tcn)
 DEFAULT_SPLIT = 1
 
 
