@@ -76,6 +76,11 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_SLEEP
 #define TCN_SLEEP 1  // s_sleep argument between poll passes (units of 64 clocks)
 #endif
+#ifndef TCN_P2W
+#define TCN_P2W 0    // every wave polls the GN2 words and finishes the moments itself (groups <= FG_WAVE): no
+                     // barrier after the res_out GEMM, so waves 0-3 run the r epilogue while 4-7 finish the GEMM;
+                     // bitwise equal, measured 4 us per forward slower (profiles/r02ax_ab_p2w.txt): off
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -774,7 +779,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
-      {
+      float fmu2 = 0.f, frs2 = 0.f;  // GN2 {mean, rstd}, wave-uniform (TCN_P2W)
+      if (TCN_P2W && TCN_GNW && G <= FG_WAVE) {
+        // lanes 4 mm + {0..3} of EVERY wave poll member mm's GN2 words; the same doubles in the same order in
+        // every wave (member_moments_w), so no LDS round trip and no barrier: d stays unread-over until the x'
+        // update, several barriers later
+        const u64* p[1] = {lane < 4 * G ? slot(lane >> 2, e2) + GW_STAT + (lane & 3) : nullptr};
+        unsigned v[1];
+        gpoll<1>(p, tag2, v, a);
+        member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], fmu2, frs2);
+      TPROBE(6);
+      } else {
         const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
         unsigned v[1];
         gpoll<1>(p, tag2, v, a);
@@ -804,7 +819,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float fmu, frs;
         {
 #if TCN_GNW
-          if (G <= FG_WAVE) {
+          if (TCN_P2W && G <= FG_WAVE) {
+            fmu = fmu2; frs = frs2;
+          } else if (G <= FG_WAVE) {
             fmu = sm.gmom[2]; frs = sm.gmom[3];
           } else {
             const double2 acc = member_sums2(sm.gw, G, lane);
