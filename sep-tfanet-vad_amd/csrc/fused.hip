@@ -81,6 +81,9 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
                      // barrier after the res_out GEMM, so waves 0-3 run the r epilogue while 4-7 finish the GEMM;
                      // bitwise equal, measured 4 us per forward slower (profiles/r02ax_ab_p2w.txt): off
 #endif
+#ifndef TCN_P3CHUNK
+#define TCN_P3CHUNK 8  // members per P3 poll pass (8: one pass up to G = 8; 16: two passes instead of four at G = 32)
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -887,8 +890,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(7);
         // consume P3: rowsums of every member (a_f), channel sums of the 4 frames either side (a_t)
         {
-          const u64* pp[FG_CHUNK];
-          unsigned v[FG_CHUNK];
+          constexpr int PC = TCN_P3CHUNK;
+          static_assert(PC >= 8, "the a_t words of the first pass");
+          const u64* pp[PC];
+          unsigned v[PC];
           int mi = -1;  // a_t input index (frame t0 - 4 + mi) served by this thread
           const u64* pat = nullptr;
           if (tid >= CH && tid < CH + 8) {
@@ -902,11 +907,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
 #endif
           }
-          // FG_CHUNK members per pass (one pass up to 8 members), summed in member order
+          // PC members per pass, summed in member order
           float s = 0.f, vat = 0.f;
-          for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
+          for (int c0 = 0; c0 < G; c0 += PC) {
 #pragma unroll
-            for (int mm = 0; mm < FG_CHUNK; ++mm)
+            for (int mm = 0; mm < PC; ++mm)
               pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
 #if TCN_COLW
             if (c0 == 0 && mi >= 0) {
@@ -916,10 +921,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #else
             if (c0 == 0 && mi >= 0) pp[0] = pat;
 #endif
-            gpoll<FG_CHUNK>(pp, tag3, v, a);
+            gpoll<PC>(pp, tag3, v, a);
             if (tid < CH) {
 #pragma unroll
-              for (int mm = 0; mm < FG_CHUNK; ++mm)
+              for (int mm = 0; mm < PC; ++mm)
                 if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
 #if TCN_COLW
