@@ -167,3 +167,24 @@ def test_vad_taps_finished_in_istft(nets):
     assert np.abs(sg.cpu().numpy() - g["sep"]).max() <= SEP_TOL
     assert np.array_equal(vg.cpu().numpy() >= 0.5, g["vad"] >= 0.5)
     assert np.abs(vg.cpu().numpy() - g["vad"]).max() <= VAD_PROB_TOL
+
+
+def test_long_files_full_chip_groups(nets, state_dicts):
+    """16 s files at B=8 (bench --workload long): 8 groups of 32 members fill the 256 CUs, each group on one
+    XCD (the L2-resident hand-off protocol), at T = 1001 (two-pass moment polls, LDS GroupNorm finish)."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    x = torch.from_numpy(synth.make_batch(8, 256000, 8080)[0])
+    sf, vf, _, used = _run(net, x.to(DEV), True)
+    assert used
+    sm, vm, _, used_m = _run(net, x.to(DEV), False)
+    assert not used_m
+    assert (sf - sm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    s_ref, v_ref, _ = om(x[:1])
+    assert np.abs(sf[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((vf[:1].cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
