@@ -84,6 +84,11 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_P3CHUNK
 #define TCN_P3CHUNK 8  // members per P3 poll pass (8: one pass up to G = 8; 16: two passes instead of four at G = 32)
 #endif
+#ifndef TCN_DWSPLIT
+#define TCN_DWSPLIT 0  // depthwise conv in two channel halves; the second half's rows are computed between the
+                       // first 8 K steps of the res_out GEMM (which read only the first half's hidden channels);
+                       // parity tests green, measured no gain (profiles/r02az_ab_dwsplit.txt; 17 VGPRs spill): off
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -274,6 +279,53 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   }
 #pragma unroll
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
+}
+
+// K steps [S0, S1) of the same GEMM (ring slot s % RD holds step s; refills while s + RD < NS), with cb(s)
+// after step s's MFMAs and refill loads: independent work placed ahead of the next step's wait on its weights.
+template <int NS, int LDA, int PRE, int S0, int S1, int RD = PD, typename CB>
+__device__ __forceinline__ void wave_gemm_rng(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
+                                              __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
+                                              u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane, CB&& cb) {
+  static_assert(NS % RD == 0 && NS >= RD && S0 % RD == 0 && S0 < S1 && S1 <= NS, "K steps");
+  constexpr bool X3 = PRE == PREC_F16X3;
+  const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
+  f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * S0);
+  f16x8 al = ah;
+  if constexpr (X3) al = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * S0);
+#pragma unroll
+  for (int s = S0; s < S1; ++s) {
+    const int i = s % RD;
+    const bool pf = s + RD < NS;
+    f16x8 nh = ah, nl = al;
+    if (s + 1 < S1) {
+      nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
+      if constexpr (X3) nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
+    }
+    if constexpr (X3) {
+      const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
+      const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+    } else if constexpr (PRE == PREC_F16) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, __builtin_bit_cast(f16x8, rh[i]), acc, 0, 0, 0);
+    } else {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, rh[i]),
+                                                    acc, 0, 0, 0);
+    }
+    if (pf) {
+      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
+      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
+    }
+    ah = nh; al = nl;
+    if (s + 1 < S1) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 : 1, 0);
+    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, X3 ? 2 : 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    cb(s);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 template <int PRE, int RD = PD>
@@ -690,6 +742,100 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         if (!TCN_PFX && !(TCN_EARLY & 2)) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
+#if TCN_DWSPLIT
+      // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))), in two channel halves:
+      // half A (input channels 0..127 -> hidden 0..255, the res_out GEMM's K steps 0..15) first, then half B's rows
+      // between K steps 0..7 of the GEMM, whose weights stream from L2 meanwhile ================
+      const unsigned e2 = ++ep, tag2 = a.tag0 + e2;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      {
+        const int cA = tid & (CH / 2 - 1), rq = wave_s / 2 * (FR / 4);  // 8 own rows per thread (wave-uniform)
+        const float a2 = pm[PB_A2];
+        float mu, rs;
+#if TCN_GNW
+        if (G <= FG_WAVE) {
+          mu = sm.gmom[0]; rs = sm.gmom[1];
+        } else {
+          const double2 acc2 = member_sums2(sm.gw, G, lane);
+          gn_moments_f(acc2.x, acc2.y, a.inv_ch, 1e-8f, mu, rs);
+        }
+#else
+        {
+          const double2 acc2 = member_sums2(sm.gw, G, lane);
+          gn_moments_f(acc2.x, acc2.y, a.inv_ch, 1e-8f, mu, rs);
+        }
+#endif
+        float st[2] = {0.f, 0.f};
+        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
+        auto half = [&](auto DC, int c, float (&hv)[FR / 4 + 8], float (&wv)[2][4]) {
+          constexpr int D = decltype(DC)::value;
+          const float sc = rs * pm[PB_G1 + c], sh = pm[PB_BE1 + c] - sc * mu;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int j = 2 * c + q;
+            wv[q][0] = pm[PB_WD + j * 3 + 0]; wv[q][1] = pm[PB_WD + j * 3 + 1]; wv[q][2] = pm[PB_WD + j * 3 + 2];
+            wv[q][3] = pm[PB_BD + j];
+          }
+#pragma unroll
+          for (int i = 0; i < FR / 4 + 2 * D; ++i) {
+            const int tl = rq - D + i, t = t0 + tl;
+            const float x = sm.H[(tl + 4) * CH + c];
+            const float vm = (t >= 0 && t < T) ? 1.f : 0.f;
+            hv[i] = fmaf(x, sc, sh) * vm;
+          }
+        };
+        auto out_row = [&](auto DC, int c, const float (&hv)[FR / 4 + 8], const float (&wv)[2][4], int i) {
+          constexpr int D = decltype(DC)::value;
+          const int tl = rq + i;
+          const float vo = t0 + tl < T ? 1.f : 0.f;
+          float dv[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            float x = wv[q][3];
+            x = fmaf(wv[q][0], hv[i], x);
+            x = fmaf(wv[q][1], hv[i + D], x);
+            x = fmaf(wv[q][2], hv[i + 2 * D], x);
+            const float v = prelu_f(x, a2) * vo;
+            st[0] += v; st[1] += v * v;
+            dv[q] = v;
+          }
+          split_store2<PRE>(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
+        };
+        auto body = [&](auto DC) {
+          float hv[FR / 4 + 8], wv[2][4];
+          half(DC, cA, hv, wv);
+#pragma unroll
+          for (int i = 0; i < FR / 4; ++i) {
+            if (TCN_PFX) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i);  // ring slot i = K step i
+            out_row(DC, cA, hv, wv, i);
+          }
+          if (!TCN_PFX) prefetch_w<PRE>(w2h, w2l, voff2, rh, rl);
+          __syncthreads();  // hidden channels 0..255 of every row in LDS
+          const int cB = cA + CH / 2;
+          float hvB[FR / 4 + 8], wvB[2][4];
+          half(DC, cB, hvB, wvB);
+          wave_gemm_rng<NS2, LDD, PRE, 0, NS2 / 2>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, rh, rl, lane, [&](int s) {
+            if (s < FR / 4) out_row(DC, cB, hvB, wvB, s);
+          });
+        };
+        switch (dil) {
+          case 1: body(std::integral_constant<int, 1>{}); break;
+          case 2: body(std::integral_constant<int, 2>{}); break;
+          case 3: body(std::integral_constant<int, 3>{}); break;
+          default: body(std::integral_constant<int, 4>{}); break;
+        }
+        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS (hidden 256..511 too)
+      }
+      TPROBE(4);
+      // ---- P2 words: GN2 partial sums (awaited after the res_out main loop) ----
+      if (tid < 2) gputd(slot(g, e2) + GW_STAT + 2 * tid, tag2, sm.dred[tid], l2);
+      {
+        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
+        wave_gemm_rng<NS2, LDD, PRE, NS2 / 2, NS2>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, rh, rl, lane, [](int) {});
+      TPROBE(5);
+      }
+#else
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
         const int c = tid & (CH - 1), rh0 = (tid >> 8) * (FR / 2);
@@ -782,6 +928,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
+#endif
       float fmu2 = 0.f, frs2 = 0.f;  // GN2 {mean, rstd}, wave-uniform (TCN_P2W)
       if (TCN_P2W && TCN_GNW && G <= FG_WAVE) {
         // lanes 4 mm + {0..3} of EVERY wave poll member mm's GN2 words; the same doubles in the same order in
