@@ -89,6 +89,11 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
                        // first 8 K steps of the res_out GEMM (which read only the first half's hidden channels);
                        // parity tests green, measured no gain (profiles/r02az_ab_dwsplit.txt; 17 VGPRs spill): off
 #endif
+#ifndef TCN_STAGGER
+#define TCN_STAGGER 0  // us of start delay for every other group of an XCD: the groups' GEMM phases (all CUs of an
+                       // XCD pull the same block weights from its L2 at once) shifted against the others' VALU phases;
+                       // measured: k_tcn longer by exactly the delay (profiles/r02az_ab_stagger.txt): off
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -533,6 +538,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (tid < FR) sm.at[tid] = 1.f;
   }
   bool l2 = false;
+  if (TCN_STAGGER > 0 && ((grp >> 3) & 1)) {  // diagnostics / A/B: bounded spin on the 100 MHz wall clock
+    const unsigned long long t_end = wall_clock64() + TCN_STAGGER * 100ull;
+    while (wall_clock64() < t_end) __builtin_amdgcn_s_sleep(8);
+  }
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
