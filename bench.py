@@ -16,9 +16,10 @@ Extra fields:
                 conv, res_out 512->256, TF-attention, recursive LN in one launch); algorithmic FLOPs per
                 launch (its two pointwise GEMMs per block) / its average launch time from HIP events that
                 libsepvad records on the stream the kernel runs on. On the multi-kernel
-                schedule (fp32 GEMMs, T > 256) the res_out GEMM.
-  cpu_baseline  the oracle CPU restatement (oracle/torch_ref.py, torch fp32) on all host cores,
-                rank 0 at N=1 only, on a bounded sample of the same workload.
+                schedule (fp32 GEMMs, T > 1024, SEPVAD_FUSED=0) the res_out GEMM.
+  cpu_baseline  the oracle CPU restatement (oracle/torch_ref.py, torch fp32) on every core of this
+                process's CPU share (the cgroup quota caps it: 16 on the GPU box, where os.cpu_count()
+                reports the whole machine), rank 0 at N=1 only, on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
