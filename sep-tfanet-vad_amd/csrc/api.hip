@@ -21,6 +21,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../../include/sepvad.h"
 #include "sepvad_internal.h"
 
@@ -884,6 +886,19 @@ struct TailProbe {
   }
 };
 
+// Host-side trace ranges (roctx: `rocprofv3 --marker-trace`), one per forward and per stage of its enqueue,
+// so a host timeline shows where the forward's launch time goes; no-ops without a tool attached.
+struct TraceRange {
+  explicit TraceRange(const char* n) { roctxRangePushA(n); }
+  void next(const char* n) {
+    roctxRangePop();
+    roctxRangePushA(n);
+  }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange&) = delete;
+  TraceRange& operator=(const TraceRange&) = delete;
+};
+
 int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b0, int B, int N,
                   const SepVadOutputs* out, const SepVadInferKw* kw, hipStream_t s, TimingRec* tr,
                   const XMap& xm) {
@@ -898,6 +913,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   const size_t g1_grid = (size_t)B * ntu * (CH / TILE);
   const bool probing = tr && h->probe && h->probe_blk >= 0;
 
+  TraceRange stage("sepvad::stft_gate");
   // 1+2. STFT (spec_output for est; spec_input for the spectrum: one transform when the windows are equal)
   // fused with the activity gate, the TCN input and the TCN.LN statistics (k_stft_gate)
   {
@@ -924,6 +940,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     }
   }
   // 3+4. TCN + output head
+  stage.next("sepvad::tcn_head");
   const int G = (T + FR - 1) / FR;
   const bool use_fused = fused_ok(h, T);
   h->last_fused = use_fused;
@@ -1123,6 +1140,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
     }
   }
+  stage.next("sepvad::vad");
   // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from k_head's tap products (k_vad_feat,
   // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
@@ -1149,6 +1167,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     HIPCHK(launch_vad1(v, s));
     HIPCHK(tp.dump(B * 2, Tp / VAD_ROWS));
   }
+  stage.next("sepvad::istft");
   // 6. VAD tail + est = X * sigmoid(mask) [* smoothed VAD] -> iSTFT (model/model.py:429-460)
   {
     IstftArgs is{};
@@ -1274,6 +1293,7 @@ int32_t sepvad_forward_strided(sepvad_handle h, const float* x, int64_t ldx, int
   if (B < 1) return fail(SEPVAD_E_SHAPE, "sepvad_forward: B must be >= 1");
   if (N <= HOP) return fail(SEPVAD_E_SHAPE, "sepvad_forward: N must exceed 256 (reflect padding of the STFT)");
   if (ldx < N || ldx > INT32_MAX) return fail(SEPVAD_E_SHAPE, "sepvad_forward: row stride must be >= N");
+  TraceRange trace("sepvad_forward");
   DeviceGuard dg(h->device);
   std::lock_guard<std::mutex> lk(h->mu);
   return forward_impl(h, x, (int)ldx, B, N, out, kw, (hipStream_t)stream);

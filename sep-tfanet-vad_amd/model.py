@@ -219,7 +219,13 @@ class SeparationModel(nn.Module):
             raise RuntimeError("SeparationModel (MI355X build) runs on a ROCm device only: "
                                "move the model and the input to 'cuda' (there is no CPU path)")
         h = self.native_handle(x.device)
-        out = h.forward(x, inference_kw if inference_kw else None)
+        # a torch.profiler range around the native forward when a profiler is active (the library adds roctx
+        # ranges per stage for rocprofv3 --marker-trace)
+        if torch.autograd._profiler_enabled():
+            with torch.profiler.record_function("sepvad.forward"):
+                out = h.forward(x, inference_kw if inference_kw else None)
+        else:
+            out = h.forward(x, inference_kw if inference_kw else None)
         self.__dict__["_side_src"] = (h, out["stream"], out["B"], out["T"])
         self.__dict__["_side_cache"] = {}
         self.estimated_stfts = out["est"]

@@ -163,3 +163,18 @@ def test_side_attributes_materialised_on_read(net):
             assert torch.equal(lazy, eager[k]), k
     net.spectrum = "user value"  # plain-attribute assignment keeps working
     assert net.spectrum == "user value"
+
+
+def test_profiler_range_around_forward():
+    """SURVEY §5 tracing: a torch.profiler range around the native forward when a profiler is active."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    net = pkg.SeparationModel(**pkg.CONFIG_WITH_VAD)
+    sd = synth.make_state_dict(pkg.CONFIG_WITH_VAD, 1234)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net = net.eval().to("cuda")
+    x = torch.from_numpy(synth.make_batch(2, 8000, 5)[0]).to("cuda")
+    with torch.no_grad(), torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        net(x)
+    torch.cuda.synchronize()
+    assert any(e.name == "sepvad.forward" for e in prof.events())

@@ -13,7 +13,8 @@ done
 wait
 for spec in "$@"; do
   name=${spec%%=*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/lib_$name.so var/fused_$name.o $objs
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/lib_$name.so var/fused_$name.o $objs \
+      -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
   rm -f var/fused_$name.o
 done
 ls -la var/
