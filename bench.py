@@ -121,6 +121,29 @@ def cpu_baseline(seconds: float = 12.0):
                        f"affinity capped by the cgroup quota; os.cpu_count() = {os.cpu_count()})")
 
 
+_JSON_FD = None
+
+
+def hold_stdout():
+    """From here on the process's fd 1 is its stderr; only emit() writes to the real stdout. Native libraries
+    print banners to fd 1 (RCCL prints its version / hostname at init on some hosts), and the driver reads
+    exactly one JSON line from rank 0's stdout."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    sys.stdout.flush()
+    if _JSON_FD is None:
+        os.write(1, line)
+    else:
+        os.write(_JSON_FD, line)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -148,7 +171,9 @@ def init_dist(args, backend="nccl"):
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     d = None
-    if world > 1:
+    # SEPVAD_BENCH_FORCE_DIST=1: the process group even at world 1 (exercises the RCCL barrier / max-reduce
+    # path of the timed region on a one-GPU box)
+    if world > 1 or os.environ.get("SEPVAD_BENCH_FORCE_DIST") == "1":
         import torch.distributed as d
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
@@ -230,7 +255,7 @@ def bench_stream(args):
                        "parallelism": f"dp{world} (stream shards; 32-byte PIT all-reduce per window)"},
             "audio_seconds_per_second": round(windows / el * save_sec, 2),
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
@@ -259,6 +284,7 @@ def main():
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
+    hold_stdout()
     if args.workload == "stream":
         return bench_stream(args)
 
@@ -402,7 +428,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline and args.workload == "offline":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
