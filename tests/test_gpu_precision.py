@@ -28,7 +28,8 @@ DEV = "cuda"
 # 9.6e-4 dB, 3.9e-3 dB, 42 / 32256; f16x3 5.1e-6, 1.6e-7 dB, 9.5e-7 dB, 0. bf16 stays inside the metric
 # string's 0.01 dB SI-SDR gate; only the fp32-equivalent arms meet the 1e-4 waveform gate.
 GATES = {"f16": (5e-4, 1e-3, 5e-3, 1e-3), "bf16": (5e-3, 5e-3, 1e-2, 1e-2), "f16x3": (1e-4, 1e-4, 1e-3, 1e-4)}
-CFGS = {"cfg2": (64, 32000), "cfg5": (128, 32000)}  # cfg 5: 128 utterances per GPU (1024 over 8)
+# cfg 5: 128 utterances per GPU (1024 over 8); long: 16 s files (T = 1001, groups of 32 workgroups)
+CFGS = {"cfg2": (64, 32000), "cfg5": (128, 32000), "long": (2, 256000)}
 
 
 @pytest.fixture(scope="module")
