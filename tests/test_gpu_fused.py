@@ -59,14 +59,17 @@ def test_fused_matches_reference_goldens(cname, case, nets):
 
 
 @pytest.mark.parametrize("cname", CONFIGS)
-@pytest.mark.parametrize("N", [2000, 8000, 12345, 32000, 48000, 64000, 96000, 140000, 200000, 261888])
+@pytest.mark.parametrize("N", [300, 2000, 8000, 12345, 32000, 48000, 64000, 96000, 140000, 200000, 261888])
 def test_fused_vs_multikernel_and_oracle(cname, N, nets, state_dicts):
-    """G = 1, 1, 2, 4, 6, 8, 12, 18, 25, 32 workgroups per utterance (G > 16: GroupNorm words finished
+    """G = 1, 1, 1, 2, 4, 6, 8, 12, 18, 25, 32 workgroups per utterance (T = 2 at the smallest) (G > 16: GroupNorm words finished
     from LDS; G > 23: the moment words polled in two passes; T = 1024 at the largest)."""
     from oracle.torch_ref import OracleModel
     from sep_tfanet_vad_amd import synth
     B = 3
-    x = torch.from_numpy(synth.make_batch(B, N, 31 + N)[0])
+    if N < 1000:  # too short for the gated synthetic sources (an all-silent mixture has no min-max scale)
+        x = torch.rand(B, N, generator=torch.Generator().manual_seed(N)) * 1.8 - 0.9
+    else:
+        x = torch.from_numpy(synth.make_batch(B, N, 31 + N)[0])
     net = nets[cname]
     sf, vf, ef, used = _run(net, x.to(DEV), True)
     assert used
