@@ -12,7 +12,9 @@ runs its own shard of utterances (weak scaling, no collective on the data path, 
 the timed region and a max-reduce of the elapsed time). Rank 0 prints one JSON line.
 
 Extra fields:
-  roofline      dominant kernel = k_tcn, the fused persistent TCN (24 blocks of conv1d 256->256, depthwise
+  roofline      (+ weight_stream: the per-CU weight bytes of the launch, their rate, and the texture-path
+                busy fraction from the committed counters — the decomposition's real floor)
+                dominant kernel = k_tcn, the fused persistent TCN (24 blocks of conv1d 256->256, depthwise
                 conv, res_out 512->256, TF-attention, recursive LN in one launch); algorithmic FLOPs per
                 launch (its two pointwise GEMMs per block) / its average launch time from HIP events that
                 libsepvad records on the stream the kernel runs on. On the multi-kernel
@@ -66,6 +68,32 @@ def tcn_bytes(B, T, precision="f16x3"):
     Tp = (T + 63) // 64 * 64
     wbytes = 4 if precision == "f16x3" else 2
     return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * wbytes
+
+
+TA_FILE = "r02as_pmc_ta_summary.txt"   # texture-path counters of k_tcn (tools/pmc_ta.sh), cfg 2, f16x3
+
+
+def weight_stream(B, T, precision, avg_launch_s, n_cu=256):
+    """The fused TCN's per-CU weight stream: every workgroup pulls every block's weights once per 32-frame
+    slice it owns, so each CU moves slices x 24 x (256x256 + 512x256) x 4 (fp16 hi/lo) or 2
+    bytes per launch. With the texture-path busy fraction from the committed counters where they apply."""
+    G = (T + 31) // 32
+    slices = -(-B * G // n_cu)
+    wbytes = 4 if precision == "f16x3" else 2
+    per_cu = slices * 24 * (256 * 256 + 256 * 512) * wbytes
+    out = {"bytes_per_cu_per_launch": per_cu, "slices_per_cu": slices,
+           "achieved_GBps_per_cu": round(per_cu / avg_launch_s / 1e9, 2), "ta_busy_frac": None, "ta_source": None}
+    path = os.path.join(REPO, "profiles", TA_FILE)
+    if precision == "f16x3" and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
+        try:
+            lines = open(path).read().splitlines()
+            i = next(k for k, ln in enumerate(lines) if "k_tcn" in ln)
+            kv = dict(t.split("=") for t in lines[i + 1].split())
+            out["ta_busy_frac"] = round(float(kv["TA_BUSY_avr"]) / (float(kv["GRBM_GUI_ACTIVE"]) / 8), 3)
+            out["ta_source"] = "profiles/" + TA_FILE + " (TA_BUSY_avr per CU / GRBM_GUI_ACTIVE per XCD)"
+        except (OSError, StopIteration, KeyError, ValueError):
+            pass
+    return out
 
 
 def res_out_bytes(B, T):
@@ -426,6 +454,8 @@ def main():
                 "gemm_share_of_forward": round(gemm_ms / tot_ms, 3) if tot_ms > 0 else None,
             },
         }
+        if fused:
+            out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s)
         if world == 1 and not args.no_cpu_baseline and args.workload == "offline":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         emit(out)
