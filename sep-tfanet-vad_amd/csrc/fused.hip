@@ -94,6 +94,9 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
                        // XCD pull the same block weights from its L2 at once) shifted against the others' VALU phases;
                        // measured: k_tcn longer by exactly the delay (profiles/r02az_ab_stagger.txt): off
 #endif
+#ifndef TCN_PD2
+#define TCN_PD2 8    // res_out weight-ring depth (its own registers when deeper than PD: the conv1d ring is dead by then)
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -345,9 +348,9 @@ __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_b
 
 // Ring entry s only (the burst above spread over a phase's rows: a CU's texture path takes one 1 KB wave load
 // per ~16 clocks, so 8 waves issuing the whole ring at once stall ~1 us on issue)
-template <int PRE>
+template <int PRE, int RD = PD>
 __device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                            u32x4v (&rh)[PD], u32x4v (&rl)[PD], int s) {
+                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD], int s) {
   rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
   if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
 }
@@ -637,6 +640,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int tido = fresh_tid(wave_s);
       const int hl4o = 4 * ((tido >> 5) & 1), mo_ = 32 * wave_s + (tido & 31);
       const int m = mo_, tid = tido, lane = tid & 63, hl = hl4o >> 2, wave = wave_s;
+      u32x4v rh2[TCN_PD2 == PD ? 1 : TCN_PD2], rl2[TCN_PD2 == PD ? 1 : TCN_PD2];  // res_out ring (TCN_PD2 > PD)
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
       if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
@@ -900,7 +904,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
-            if (TCN_PFX && !(TCN_EARLY & 2) && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
+            if constexpr (TCN_PD2 == PD) {
+              if (TCN_PFX && !(TCN_EARLY & 2) && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
+            } else {
+              static_assert(TCN_PD2 == 2 * PD, "one res_out ring entry per dwconv row");
+              prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, i);
+            }
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -934,7 +943,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
+        if constexpr (TCN_PD2 == PD)
+          wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
+        else
+          wave_gemm<NS2, LDD, PRE, TCN_PD2>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh2,
+                                            rl2, lane);
       TPROBE(5);
       }
 #endif
