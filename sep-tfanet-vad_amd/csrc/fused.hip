@@ -97,6 +97,9 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_PD2
 #define TCN_PD2 8    // res_out weight-ring depth (its own registers when deeper than PD: the conv1d ring is dead by then)
 #endif
+#ifndef TCN_PD2LATE
+#define TCN_PD2LATE 0  // with TCN_PD2 = 16: only slots 0..7 during the dwconv, slots 8..15 issued at the GEMM's start
+#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -906,6 +909,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
             if constexpr (TCN_PD2 == PD) {
               if (TCN_PFX && !(TCN_EARLY & 2) && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
+            } else if constexpr (TCN_PD2LATE) {
+              if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, i / 2);
             } else {
               static_assert(TCN_PD2 == 2 * PD, "one res_out ring entry per dwconv row");
               prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, i);
@@ -945,9 +950,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       {
         if constexpr (TCN_PD2 == PD)
           wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
-        else
+        else {
+          if constexpr (TCN_PD2LATE) {  // the second half of the deep ring, in flight from the GEMM's start
+            const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
+#pragma unroll
+            for (int k = TCN_PD2 / 2; k < TCN_PD2; ++k) prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, k);
+          }
           wave_gemm<NS2, LDD, PRE, TCN_PD2>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh2,
                                             rl2, lane);
+        }
       TPROBE(5);
       }
 #endif
