@@ -60,46 +60,6 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_PFX
 #define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
 #endif
-#ifndef TCN_EARLY
-#define TCN_EARLY 0  // bit 0: next block's conv1d weight ring issued with the res_out epilogue rows (else the x' update
-                     // rows); bit 1: the res_out weight ring with the conv1d epilogue rows (else the dwconv rows)
-#endif
-#ifndef TCN_MED3
-#define TCN_MED3 0   // PReLU as med3(x, a x, +-inf) (prelu_m): off — it stops hipcc's SLP packing of the dwconv
-                     // (static VALU 3798 -> 4403) and measured within noise (profiles/r02ar_ab_early.txt)
-#endif
-#ifndef TCN_COLW
-#define TCN_COLW 0   // P3 frame sums: the 8 boundary frames' per-wave partials published from registers before the
-                     // barrier (consumers add the 8 wave partials in wave order: the same bits as the summed word);
-                     // bitwise equal, but measured 17 us per forward slower (profiles/r02au_ab_colw.txt): off
-#endif
-#ifndef TCN_SLEEP
-#define TCN_SLEEP 1  // s_sleep argument between poll passes (units of 64 clocks)
-#endif
-#ifndef TCN_P2W
-#define TCN_P2W 0    // every wave polls the GN2 words and finishes the moments itself (groups <= FG_WAVE): no
-                     // barrier after the res_out GEMM, so waves 0-3 run the r epilogue while 4-7 finish the GEMM;
-                     // bitwise equal, measured 4 us per forward slower (profiles/r02ax_ab_p2w.txt): off
-#endif
-#ifndef TCN_P3CHUNK
-#define TCN_P3CHUNK 8  // members per P3 poll pass (8: one pass up to G = 8; 16: two passes instead of four at G = 32)
-#endif
-#ifndef TCN_DWSPLIT
-#define TCN_DWSPLIT 0  // depthwise conv in two channel halves; the second half's rows are computed between the
-                       // first 8 K steps of the res_out GEMM (which read only the first half's hidden channels);
-                       // parity tests green, measured no gain (profiles/r02az_ab_dwsplit.txt; 17 VGPRs spill): off
-#endif
-#ifndef TCN_STAGGER
-#define TCN_STAGGER 0  // us of start delay for every other group of an XCD: the groups' GEMM phases (all CUs of an
-                       // XCD pull the same block weights from its L2 at once) shifted against the others' VALU phases;
-                       // measured: k_tcn longer by exactly the delay (profiles/r02az_ab_stagger.txt): off
-#endif
-#ifndef TCN_PD2
-#define TCN_PD2 8    // res_out weight-ring depth (its own registers when deeper than PD: the conv1d ring is dead by then)
-#endif
-#ifndef TCN_PD2LATE
-#define TCN_PD2LATE 0  // with TCN_PD2 = 16: only slots 0..7 during the dwconv, slots 8..15 issued at the GEMM's start
-#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -118,7 +78,7 @@ constexpr int LDX = CH + 8;       // x' row stride (halves): 132 dwords == 4 (mo
 constexpr int LDD = HID + 8;      // d row stride (halves): 260 dwords == 4 (mod 64)
 constexpr int HROW = FR + 8;      // conv1d output rows incl. 4 halo rows on each side
 #ifndef TCN_PD
-#define TCN_PD 8
+#define TCN_PD 8     // weight K steps in flight per wave (4: +10 us; 16: spills at 2 waves per SIMD)
 #endif
 constexpr int PD = TCN_PD;        // weight K steps in flight per wave
 constexpr int NS1 = CH / 16;      // conv1d K steps (256 / 16)
@@ -141,14 +101,6 @@ struct TcnSmem {
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
-
-// PReLU x > 0 ? x : a x (torch) as one v_med3 of x, a x and a bound chosen once per slope: for a <= 1 it is
-// max(x, a x) (bound +inf), for a > 1 min(x, a x) (bound -inf). Returns one of the two operands (the same value
-// as prelu_f for every finite x; the surrounding code generation, and so the rounding of later sums, differs).
-__device__ __forceinline__ float prelu_bound(float a) { return a <= 1.f ? __builtin_inff() : -__builtin_inff(); }
-__device__ __forceinline__ float prelu_m(float x, float a, float bound) {
-  return __builtin_amdgcn_fmed3f(x, a * x, bound);
-}
 
 // Wave-uniform copies (readfirstlane) of values loaded from the block-parameter table: the compiler cannot
 // prove those loads uniform, and a buffer descriptor in VGPRs becomes a waterfall loop per access.
@@ -211,7 +163,7 @@ __device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, un
       }
     }
     if (ok) return;
-    __builtin_amdgcn_s_sleep(TCN_SLEEP);
+    __builtin_amdgcn_s_sleep(1);
     if ((++spins & 255u) == 0 &&
         (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
       giveup(a);
@@ -224,7 +176,7 @@ constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq h
 constexpr int GW_TOP = 4;           // P1: rows 0..dil-1      [dil][256]
 constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
 constexpr int GW_ROW = 0;           // P3: per-channel sums over own frames [256]
-constexpr int GW_COL = CH;          // P3: per-frame channel sums [32] (TCN_COLW: boundary frames' wave partials [8][8])
+constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
 static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
@@ -292,53 +244,6 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
 }
 
-// K steps [S0, S1) of the same GEMM (ring slot s % RD holds step s; refills while s + RD < NS), with cb(s)
-// after step s's MFMAs and refill loads: independent work placed ahead of the next step's wait on its weights.
-template <int NS, int LDA, int PRE, int S0, int S1, int RD = PD, typename CB>
-__device__ __forceinline__ void wave_gemm_rng(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
-                                              __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                              u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane, CB&& cb) {
-  static_assert(NS % RD == 0 && NS >= RD && S0 % RD == 0 && S0 < S1 && S1 <= NS, "K steps");
-  constexpr bool X3 = PRE == PREC_F16X3;
-  const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
-  f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * S0);
-  f16x8 al = ah;
-  if constexpr (X3) al = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * S0);
-#pragma unroll
-  for (int s = S0; s < S1; ++s) {
-    const int i = s % RD;
-    const bool pf = s + RD < NS;
-    f16x8 nh = ah, nl = al;
-    if (s + 1 < S1) {
-      nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
-      if constexpr (X3) nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
-    }
-    if constexpr (X3) {
-      const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
-      const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-    } else if constexpr (PRE == PREC_F16) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, __builtin_bit_cast(f16x8, rh[i]), acc, 0, 0, 0);
-    } else {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, rh[i]),
-                                                    acc, 0, 0, 0);
-    }
-    if (pf) {
-      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
-      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
-    }
-    ah = nh; al = nl;
-    if (s + 1 < S1) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 : 1, 0);
-    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, X3 ? 2 : 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    cb(s);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 template <int PRE, int RD = PD>
 __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD]) {
@@ -351,9 +256,9 @@ __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_b
 
 // Ring entry s only (the burst above spread over a phase's rows: a CU's texture path takes one 1 KB wave load
 // per ~16 clocks, so 8 waves issuing the whole ring at once stall ~1 us on issue)
-template <int PRE, int RD = PD>
+template <int PRE>
 __device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD], int s) {
+                                            u32x4v (&rh)[PD], u32x4v (&rl)[PD], int s) {
   rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
   if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
 }
@@ -544,10 +449,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (tid < FR) sm.at[tid] = 1.f;
   }
   bool l2 = false;
-  if (TCN_STAGGER > 0 && ((grp >> 3) & 1)) {  // diagnostics / A/B: bounded spin on the 100 MHz wall clock
-    const unsigned long long t_end = wall_clock64() + TCN_STAGGER * 100ull;
-    while (wall_clock64() < t_end) __builtin_amdgcn_s_sleep(8);
-  }
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
@@ -643,7 +544,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int tido = fresh_tid(wave_s);
       const int hl4o = 4 * ((tido >> 5) & 1), mo_ = 32 * wave_s + (tido & 31);
       const int m = mo_, tid = tido, lane = tid & 63, hl = hl4o >> 2, wave = wave_s;
-      u32x4v rh2[TCN_PD2 == PD ? 1 : TCN_PD2], rl2[TCN_PD2 == PD ? 1 : TCN_PD2];  // res_out ring (TCN_PD2 > PD)
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
       if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
@@ -692,13 +592,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         u64* s1 = slot(g, e1);
         float st[2] = {0.f, 0.f};
-        const float pb1 = prelu_bound(a1);
-        const __amdgpu_buffer_rsrc_t w2he = rsrc_of(wb + WL::W2H), w2le = rsrc_of(wb + WL::W2L);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if ((TCN_EARLY & 2) && r % 2 == 0) prefetch_w1<PRE>(w2he, w2le, voff2, rh, rl, r / 2);
           const int tl = trow(r);
-          float v = TCN_MED3 ? prelu_m(fmaf(acc[r], ws, bias), a1, pb1) : prelu_f(fmaf(acc[r], ws, bias), a1);
+          float v = prelu_f(fmaf(acc[r], ws, bias), a1);
           v = (t0 + tl < T) ? v : 0.f;
           sm.H[(tl + 4) * CH + m] = v;
           st[0] += v; st[1] += v * v;
@@ -755,107 +652,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        if (!TCN_PFX && !(TCN_EARLY & 2)) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
+        if (!TCN_PFX) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
-#if TCN_DWSPLIT
-      // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))), in two channel halves:
-      // half A (input channels 0..127 -> hidden 0..255, the res_out GEMM's K steps 0..15) first, then half B's rows
-      // between K steps 0..7 of the GEMM, whose weights stream from L2 meanwhile ================
-      const unsigned e2 = ++ep, tag2 = a.tag0 + e2;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      {
-        const int cA = tid & (CH / 2 - 1), rq = wave_s / 2 * (FR / 4);  // 8 own rows per thread (wave-uniform)
-        const float a2 = pm[PB_A2];
-        float mu, rs;
-#if TCN_GNW
-        if (G <= FG_WAVE) {
-          mu = sm.gmom[0]; rs = sm.gmom[1];
-        } else {
-          const double2 acc2 = member_sums2(sm.gw, G, lane);
-          gn_moments_f(acc2.x, acc2.y, a.inv_ch, 1e-8f, mu, rs);
-        }
-#else
-        {
-          const double2 acc2 = member_sums2(sm.gw, G, lane);
-          gn_moments_f(acc2.x, acc2.y, a.inv_ch, 1e-8f, mu, rs);
-        }
-#endif
-        float st[2] = {0.f, 0.f};
-        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
-        auto half = [&](auto DC, int c, float (&hv)[FR / 4 + 8], float (&wv)[2][4]) {
-          constexpr int D = decltype(DC)::value;
-          const float sc = rs * pm[PB_G1 + c], sh = pm[PB_BE1 + c] - sc * mu;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int j = 2 * c + q;
-            wv[q][0] = pm[PB_WD + j * 3 + 0]; wv[q][1] = pm[PB_WD + j * 3 + 1]; wv[q][2] = pm[PB_WD + j * 3 + 2];
-            wv[q][3] = pm[PB_BD + j];
-          }
-#pragma unroll
-          for (int i = 0; i < FR / 4 + 2 * D; ++i) {
-            const int tl = rq - D + i, t = t0 + tl;
-            const float x = sm.H[(tl + 4) * CH + c];
-            const float vm = (t >= 0 && t < T) ? 1.f : 0.f;
-            hv[i] = fmaf(x, sc, sh) * vm;
-          }
-        };
-        auto out_row = [&](auto DC, int c, const float (&hv)[FR / 4 + 8], const float (&wv)[2][4], int i) {
-          constexpr int D = decltype(DC)::value;
-          const int tl = rq + i;
-          const float vo = t0 + tl < T ? 1.f : 0.f;
-          float dv[2];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            float x = wv[q][3];
-            x = fmaf(wv[q][0], hv[i], x);
-            x = fmaf(wv[q][1], hv[i + D], x);
-            x = fmaf(wv[q][2], hv[i + 2 * D], x);
-            const float v = prelu_f(x, a2) * vo;
-            st[0] += v; st[1] += v * v;
-            dv[q] = v;
-          }
-          split_store2<PRE>(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
-        };
-        auto body = [&](auto DC) {
-          float hv[FR / 4 + 8], wv[2][4];
-          half(DC, cA, hv, wv);
-#pragma unroll
-          for (int i = 0; i < FR / 4; ++i) {
-            if (TCN_PFX) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i);  // ring slot i = K step i
-            out_row(DC, cA, hv, wv, i);
-          }
-          if (!TCN_PFX) prefetch_w<PRE>(w2h, w2l, voff2, rh, rl);
-          __syncthreads();  // hidden channels 0..255 of every row in LDS
-          const int cB = cA + CH / 2;
-          float hvB[FR / 4 + 8], wvB[2][4];
-          half(DC, cB, hvB, wvB);
-          wave_gemm_rng<NS2, LDD, PRE, 0, NS2 / 2>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, rh, rl, lane, [&](int s) {
-            if (s < FR / 4) out_row(DC, cB, hvB, wvB, s);
-          });
-        };
-        switch (dil) {
-          case 1: body(std::integral_constant<int, 1>{}); break;
-          case 2: body(std::integral_constant<int, 2>{}); break;
-          case 3: body(std::integral_constant<int, 3>{}); break;
-          default: body(std::integral_constant<int, 4>{}); break;
-        }
-        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS (hidden 256..511 too)
-      }
-      TPROBE(4);
-      // ---- P2 words: GN2 partial sums (awaited after the res_out main loop) ----
-      if (tid < 2) gputd(slot(g, e2) + GW_STAT + 2 * tid, tag2, sm.dred[tid], l2);
-      {
-        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
-        wave_gemm_rng<NS2, LDD, PRE, NS2 / 2, NS2>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, rh, rl, lane, [](int) {});
-      TPROBE(5);
-      }
-#else
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
         const int c = tid & (CH - 1), rh0 = (tid >> 8) * (FR / 2);
-        const float a2 = pm[PB_A2], pb2 = prelu_bound(a2);
+        const float a2 = pm[PB_A2];
         // GN1 affine of this thread's channel, computed in-thread from the members' sums (member order,
         // as gn_affine: no LDS round trip, no barrier)
         float sc, sh;
@@ -907,14 +710,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
-            if constexpr (TCN_PD2 == PD) {
-              if (TCN_PFX && !(TCN_EARLY & 2) && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
-            } else if constexpr (TCN_PD2LATE) {
-              if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, i / 2);
-            } else {
-              static_assert(TCN_PD2 == 2 * PD, "one res_out ring entry per dwconv row");
-              prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, i);
-            }
+            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -924,7 +720,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               x = fmaf(wv[q][0], hv[i], x);
               x = fmaf(wv[q][1], hv[i + D], x);
               x = fmaf(wv[q][2], hv[i + 2 * D], x);
-              const float v = (TCN_MED3 ? prelu_m(x, a2, pb2) : prelu_f(x, a2)) * vo;
+              const float v = prelu_f(x, a2) * vo;
               st[0] += v; st[1] += v * v;
               dv[q] = v;
             }
@@ -948,31 +744,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        if constexpr (TCN_PD2 == PD)
-          wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
-        else {
-          if constexpr (TCN_PD2LATE) {  // the second half of the deep ring, in flight from the GEMM's start
-            const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
-#pragma unroll
-            for (int k = TCN_PD2 / 2; k < TCN_PD2; ++k) prefetch_w1<PRE, TCN_PD2>(w2h, w2l, voff2, rh2, rl2, k);
-          }
-          wave_gemm<NS2, LDD, PRE, TCN_PD2>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh2,
-                                            rl2, lane);
-        }
+        wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
-#endif
-      float fmu2 = 0.f, frs2 = 0.f;  // GN2 {mean, rstd}, wave-uniform (TCN_P2W)
-      if (TCN_P2W && TCN_GNW && G <= FG_WAVE) {
-        // lanes 4 mm + {0..3} of EVERY wave poll member mm's GN2 words; the same doubles in the same order in
-        // every wave (member_moments_w), so no LDS round trip and no barrier: d stays unread-over until the x'
-        // update, several barriers later
-        const u64* p[1] = {lane < 4 * G ? slot(lane >> 2, e2) + GW_STAT + (lane & 3) : nullptr};
-        unsigned v[1];
-        gpoll<1>(p, tag2, v, a);
-        member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], fmu2, frs2);
-      TPROBE(6);
-      } else {
+      {
         const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
         unsigned v[1];
         gpoll<1>(p, tag2, v, a);
@@ -994,17 +769,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       f32x16v& rv = acc;  // r = res_out output, in place
       const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
-      // next block's conv1d weights (the last block re-reads its own weights: the loads stay unconditional
-      // and in bounds)
-      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
-      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
       {
         float fmu, frs;
         {
 #if TCN_GNW
-          if (TCN_P2W && G <= FG_WAVE) {
-            fmu = fmu2; frs = frs2;
-          } else if (G <= FG_WAVE) {
+          if (G <= FG_WAVE) {
             fmu = sm.gmom[2]; frs = sm.gmom[3];
           } else {
             const double2 acc = member_sums2(sm.gw, G, lane);
@@ -1026,7 +795,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = trow(r);
           rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
           const float rm = t0 + tl < T ? rv[r] : 0.f;
-          if ((TCN_EARLY & 1) && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
           rsum += rm;
           csr[r] = half_total(rm);  // this frame's sum over the wave's 32 channels (lanes 31 / 63)
         }
@@ -1034,19 +802,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if ((lane & 31) == 31) {  // one branch for the 16 frame sums
 #pragma unroll
             for (int r = 0; r < 16; ++r) sm.cs[trow(r)][wave] = csr[r];
-#if TCN_COLW
-            // P3 words: the per-wave partial channel sums of the frames the neighbours read (a_t), straight from
-            // registers: lane 31 holds frames 0..3 (r = 0..3), lane 63 frames 28..31 (r = 12..15); word
-            // GW_COL + 8 * idx + wave, idx = frame (0..3) or 4 + frame - 28
-            u64* const sc = slot(g, e3) + GW_COL + wave;
-            if (hl == 0) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) gputf(sc + 8 * r, tag3, csr[r], l2);
-            } else {
-#pragma unroll
-              for (int r = 12; r < 16; ++r) gputf(sc + 8 * (r - 8), tag3, csr[r], l2);
-            }
-#endif
           }
           // P3 words: per-channel sums over own frames (a_f)
           rsum += __shfl_xor(rsum, 32);
@@ -1056,7 +811,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // ---- TF_Attention (model/model.py:182-208) ----
       if (TCN_SUB == 3) TPROBE(13);
       if (tf) {
-#if !TCN_COLW
         __syncthreads();
         if (TCN_SUB == 3) TPROBE(14);
         if (tid < FR) {  // P3 words: per-frame channel sums (a_t)
@@ -1066,55 +820,33 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sm.csum[tid] = s;
           gputf(slot(g, e3) + GW_COL + tid, tag3, s, l2);
         }
-#endif
       TPROBE(7);
         // consume P3: rowsums of every member (a_f), channel sums of the 4 frames either side (a_t)
         {
-          constexpr int PC = TCN_P3CHUNK;
-          static_assert(PC >= 8, "the a_t words of the first pass");
-          const u64* pp[PC];
-          unsigned v[PC];
+          const u64* pp[FG_CHUNK];
+          unsigned v[FG_CHUNK];
           int mi = -1;  // a_t input index (frame t0 - 4 + mi) served by this thread
           const u64* pat = nullptr;
           if (tid >= CH && tid < CH + 8) {
             const int k = tid - CH;
             mi = k < 4 ? k : FR + k;             // 0..3 and 36..39
             const int tl = mi - 4, t = t0 + tl;
-#if TCN_COLW
-            static_assert(FG_CHUNK == NTHR / 64, "one poll slot per wave partial");
-            if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + 8 * (tl + 8) : slot(g + 1, e3) + GW_COL + 8 * (tl - FR);
-#else
             if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
-#endif
           }
-          // PC members per pass, summed in member order
+          // FG_CHUNK members per pass (one pass up to 8 members), summed in member order
           float s = 0.f, vat = 0.f;
-          for (int c0 = 0; c0 < G; c0 += PC) {
+          for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
 #pragma unroll
-            for (int mm = 0; mm < PC; ++mm)
+            for (int mm = 0; mm < FG_CHUNK; ++mm)
               pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
-#if TCN_COLW
-            if (c0 == 0 && mi >= 0) {
-#pragma unroll
-              for (int w = 0; w < FG_CHUNK; ++w) pp[w] = pat != nullptr ? pat + w : nullptr;
-            }
-#else
             if (c0 == 0 && mi >= 0) pp[0] = pat;
-#endif
-            gpoll<PC>(pp, tag3, v, a);
+            gpoll<FG_CHUNK>(pp, tag3, v, a);
             if (tid < CH) {
 #pragma unroll
-              for (int mm = 0; mm < PC; ++mm)
+              for (int mm = 0; mm < FG_CHUNK; ++mm)
                 if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
-#if TCN_COLW
-            if (c0 == 0 && pat != nullptr) {  // the 8 wave partials in wave order (as the producer's csum)
-#pragma unroll
-              for (int w = 0; w < FG_CHUNK; ++w) vat += __builtin_bit_cast(float, v[w]);
-            }
-#else
             if (c0 == 0 && pat != nullptr) vat = __builtin_bit_cast(float, v[0]);
-#endif
           }
           __syncthreads();  // csum complete (read below by other threads)
           if (tid < CH) {
@@ -1124,14 +856,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             sm.mC[mi] = vat / (float)CH;
           } else if (tid >= CH + 8 && tid < CH + 8 + FR) {
             const int tl = tid - CH - 8;
-#if TCN_COLW
-            float cs = 0.f;
-#pragma unroll
-            for (int sl = 0; sl < 8; ++sl) cs += sm.cs[tl][sl];
-            sm.mC[tl + 4] = (t0 + tl < T) ? cs / (float)CH : 0.f;
-#else
             sm.mC[tl + 4] = (t0 + tl < T) ? sm.csum[tl] / (float)CH : 0.f;
-#endif
           }
         }
         __syncthreads();
@@ -1278,15 +1003,18 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
       if (TCN_SUB == 0) TPROBE(13);
       }
-      // next block's conv1d weights: in flight during the x' update (TCN_EARLY: since the res_out epilogue)
-      if (!TCN_PFX && !(TCN_EARLY & 1) && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
+      // next block's conv1d weights: in flight during the x' update
+      // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
+      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
+      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
+      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (TCN_PFX && !(TCN_EARLY & 1) && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
+          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
