@@ -71,6 +71,8 @@ def tcn_bytes(B, T, precision="f16x3"):
 
 
 TA_FILE = "r02as_pmc_ta_summary.txt"   # texture-path counters of k_tcn (tools/pmc_ta.sh), cfg 2, f16x3
+RING_FILE = "r02bi_ring_gemm.txt"       # GEMM-phase stream floor per CU (tools/probe_src/ring_gemm.hip)
+STREAM_FLOOR_GBPS = 103.2
 
 
 def weight_stream(B, T, precision, avg_launch_s, n_cu=256):
@@ -81,8 +83,11 @@ def weight_stream(B, T, precision, avg_launch_s, n_cu=256):
     slices = -(-B * G // n_cu)
     wbytes = 4 if precision == "f16x3" else 2
     per_cu = slices * 24 * (256 * 256 + 256 * 512) * wbytes
-    out = {"bytes_per_cu_per_launch": per_cu, "slices_per_cu": slices,
-           "achieved_GBps_per_cu": round(per_cu / avg_launch_s / 1e9, 2), "ta_busy_frac": None, "ta_source": None}
+    rate = per_cu / avg_launch_s / 1e9
+    out = {"bytes_per_cu_per_launch": per_cu, "slices_per_cu": slices, "achieved_GBps_per_cu": round(rate, 2),
+           # the same two GEMMs streamed back to back with nothing else (tools/probe_src/ring_gemm.hip)
+           "floor_GBps_per_cu": STREAM_FLOOR_GBPS, "frac_of_floor": round(rate / STREAM_FLOOR_GBPS, 3),
+           "floor_source": "profiles/" + RING_FILE, "ta_busy_frac": None, "ta_source": None}
     path = os.path.join(REPO, "profiles", TA_FILE)
     if precision == "f16x3" and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
         try:
