@@ -60,10 +60,6 @@ typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 #ifndef TCN_PFX
 #define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
 #endif
-#ifndef TCN_STAGE
-#define TCN_STAGE 0  // next block's conv1d K steps 8..10 of every wave staged into free LDS by waves 5-7 during the
-                     // attention phases (the weight stream is otherwise idle there): 3 fewer K steps streamed in the GEMM
-#endif
 #ifndef TCN_GNW
 #define TCN_GNW 1    // GN1/GN2 moments finished by the polling wave before the barrier (1) or by every thread after it
 #endif
@@ -104,9 +100,6 @@ struct TcnSmem {
   unsigned gw[FG_MAX * 2 * NMOM] __attribute__((aligned(8)));  // gathered statistic words of all members
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
-#if TCN_STAGE
-  u32x4v stg[16 * 64];            // staged conv1d weight slots 32..47 (slots 0..31: the A planes' upper halves)
-#endif
 };
 
 // Wave-uniform copies (readfirstlane) of values loaded from the block-parameter table: the compiler cannot
@@ -200,46 +193,13 @@ struct WLay {
 // static register ring; the first PD steps are already in (rh, rl) on entry.
 // PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
 // hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
-// NSTG > 0: K steps [RD, RD + NSTG) take their weight fragments from LDS (stg[2k], stg[2k + 1]: this lane's
-// 16 B of the hi / lo plane of staged step k), read one step ahead; the ring then refills only the steps after them.
-template <int NS, int LDA, int PRE, int RD = PD, int NSTG = 0>
+template <int NS, int LDA, int PRE, int RD = PD>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                          u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane,
-                                          const u32x4v* const* stg = nullptr) {
+                                          u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
   static_assert(NS % RD == 0 && NS >= RD, "K steps");
-  static_assert(NSTG == 0 || (NS == 2 * RD && NSTG < RD && PRE == PREC_F16X3), "staged steps: conv1d, fp16x3");
   constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
-  if constexpr (NSTG > 0) {
-    f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff), al = *reinterpret_cast<const f16x8*>(Alo + aoff);
-    u32x4v sh = rh[0], sl = rl[0];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const bool from_lds = s >= RD && s < RD + NSTG;
-      const int i = s % RD;
-      const bool pf = s + RD < NS && s + RD >= RD + NSTG;
-      f16x8 nh = ah, nl = al;
-      if (s + 1 < NS) {  // next step's A fragments (and staged B fragments) in flight during this step
-        nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
-        nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
-      }
-      u32x4v nsh = sh, nsl = sl;
-      if (s + 1 >= RD && s + 1 < RD + NSTG) { nsh = stg[2 * (s + 1 - RD)][lane]; nsl = stg[2 * (s + 1 - RD) + 1][lane]; }
-      const f16x8 bh = __builtin_bit_cast(f16x8, from_lds ? sh : rh[i]);
-      const f16x8 bl = __builtin_bit_cast(f16x8, from_lds ? sl : rl[i]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-      if (pf) {
-        rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
-        rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
-      }
-      ah = nh; al = nl; sh = nsh; sl = nsl;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    return;
-  }
   // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
   f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff);
   f16x8 al = ah;
@@ -476,18 +436,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // hand-off slots of this group: member mm, epoch e -> NGR words; tags a.tag0 + epoch
   u64* const gbase = a.gran + (size_t)grp * G * 2 * NGR;
   auto slot = [&](int mm, unsigned e) -> u64* { return gbase + ((size_t)mm * 2 + (e & 1)) * NGR; };
-#if TCN_STAGE
-  // staged conv1d weight slot q (1 KB: one wave's hi or lo plane of one K step): 0..15 in Ahi's upper half,
-  // 16..31 in Alo's (x' uses only the first FR x LDX halves of each), 32..47 in sm.stg; wave w's staged step k,
-  // plane p is slot 2 NSTG w + 2 k + p
-  constexpr int NSTG = 3;
-  static_assert(FR * LDX * 2 + 16 * 1024 == FR * LDD * 2 && 8 * 2 * NSTG == 48, "staging slots");
-  auto stg_slot = [&](int q) -> u32x4v* {
-    return q < 16 ? reinterpret_cast<u32x4v*>(reinterpret_cast<char*>(sm.Ahi) + FR * LDX * 2 + q * 1024)
-         : q < 32 ? reinterpret_cast<u32x4v*>(reinterpret_cast<char*>(sm.Alo) + FR * LDX * 2 + (q - 16) * 1024)
-                  : sm.stg + (q - 32) * 64;
-  };
-#endif
   unsigned ep = 1;  // epochs published so far (identical sequence in every member); epoch 1 = XCD ids
   // epoch 1: the members' XCD ids (write-through); if the whole group shares one XCD, every later
   // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
@@ -627,15 +575,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-#if TCN_STAGE
-        if (PRE == PREC_F16X3 && bi > 0) {  // K steps 8..10 staged in LDS during the previous block
-          const u32x4v* sp[2 * NSTG];
-#pragma unroll
-          for (int k = 0; k < 2 * NSTG; ++k) sp[k] = stg_slot(wave_s * 2 * NSTG + k);
-          if constexpr (PRE == PREC_F16X3)
-            wave_gemm<NS1, LDX, PRE, PD, NSTG>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, rh, rl, lane, sp);
-        } else
-#endif
         wave_gemm<NS1, LDX, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, rh, rl, lane);
       TPROBE(1);
       }
@@ -849,21 +788,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
 #endif
         }
-#if TCN_STAGE
-        // waves 5-7 (no polls until P4... none in P3/P4) pull the next block's conv1d K steps 8..10 of every wave
-        // into their free ring registers; written to LDS in the attention phase below
-        if (PRE == PREC_F16X3 && bi + 1 < a.nblk && wave_s >= 5) {
-          const __half* wnx = wb + WL::BLOCK;
-          const __amdgpu_buffer_rsrc_t sh_ = rsrc_of(wnx), sl_ = rsrc_of(wnx + WL::W1L);
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int q = (wave_s - 5) * 16 + j, w = q / (2 * NSTG), k = (q % (2 * NSTG)) / 2;
-            const u32x4v x = __builtin_amdgcn_raw_buffer_load_b128((q & 1) ? sl_ : sh_, (w * NS1 * 64 + lane) * 16,
-                                                                   (PD + k) * 1024, 0);
-            if (j < 8) rh[j] = x; else rl[j - 8] = x;
-          }
-        }
-#endif
         const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
         float rsum = 0.f, csr[16];
 #pragma unroll
@@ -937,12 +861,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         __syncthreads();
       TPROBE(8);
-#if TCN_STAGE
-        if (PRE == PREC_F16X3 && bi + 1 < a.nblk && wave_s >= 5) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) stg_slot((wave_s - 5) * 16 + j)[lane] = j < 8 ? rh[j] : rl[j - 8];
-        }
-#endif
         const float* p = pm + PB_ATT;
         // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the channel axis);
         // a_t: mean over channels -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the frame axis)
@@ -985,12 +903,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
         }
       }
-#if TCN_STAGE
-      if (!tf && PRE == PREC_F16X3 && bi + 1 < a.nblk && wave_s >= 5) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) stg_slot((wave_s - 5) * 16 + j)[lane] = j < 8 ? rh[j] : rl[j - 8];
-      }
-#endif
       float kc[4] = {0.f, 0.f, 0.f, 0.f};  // this channel's residual-LN affines (GN_a: 0, 1; GN_b: 2, 3)
       if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
         // moment record of u = o + r' (r' = r a_f a_t), see device_common.h recursive_affine
