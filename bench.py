@@ -204,6 +204,11 @@ def init_dist(args, backend="nccl"):
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     d = None
+    # SEPVAD_BENCH_SHARE_GPU=1 (tests only): every rank on cuda:0 with a gloo process group, so the N-rank launcher,
+    # the barrier / max-reduce and the stream PIT all-reduce run end to end on a one-GPU box (RCCL needs a GPU per
+    # rank); timing from this mode is not a scaling measurement
+    if os.environ.get("SEPVAD_BENCH_SHARE_GPU") == "1":
+        backend, local_rank = "gloo", 0
     # SEPVAD_BENCH_FORCE_DIST=1: the process group even at world 1 (exercises the RCCL barrier / max-reduce
     # path of the timed region on a one-GPU box)
     if world > 1 or os.environ.get("SEPVAD_BENCH_FORCE_DIST") == "1":
@@ -214,6 +219,11 @@ def init_dist(args, backend="nccl"):
         else:
             d.init_process_group(backend)
     return d, world, rank, local_rank
+
+
+def _reduce_dev(dist, dev):
+    """Device of the max-over-ranks reduction: the GPU under RCCL, the host under gloo."""
+    return "cpu" if dist is not None and dist.get_backend() == "gloo" else dev
 
 
 def timed_region(step, steps, warmup, dist=None, sync=lambda: None, reduce_device="cpu"):
@@ -259,7 +269,7 @@ def bench_stream(args):
         net = pkg.SeparationModel(**cfg)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_state_dict(cfg, 1234).items()}, strict=True)
     net = net.eval().to(dev)
-    n_streams, n_total, save_sec = 256, 64000, 0.16
+    n_streams, n_total, save_sec = args.batch or 256, 64000, 0.16
     x = torch.from_numpy(synth.make_batch(n_streams, n_total, 20_000 + rank * n_streams)[0]).to(dev)
     net.native_handle(dev).reserve(n_streams, 48000)
     crit = pkg.PITLossWrapper(loss_func=torch.nn.L1Loss(), pit_from="pw_pt")
@@ -273,7 +283,9 @@ def bench_stream(args):
     def step():
         ons.calc_online(x, "bench", 10 ** 6, ikw, process_group=group)
 
-    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev)
+    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, _reduce_dev(dist, dev))
+    if os.environ.get("SEPVAD_BENCH_DUMP"):  # tests: this rank's stitched streams after the last step
+        np.save(f"{os.environ['SEPVAD_BENCH_DUMP']}.rank{rank}.npy", ons.online_signal.cpu().numpy())
     if rank == 0:
         windows = world * n_streams * n_win * args.steps
         out = {
@@ -357,7 +369,7 @@ def main():
             return net(x)
 
     # timed region (value)
-    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev)
+    el = timed_region(step, args.steps, args.warmup, dist, torch.cuda.synchronize, _reduce_dev(dist, dev))
 
     # per-kernel timing pass (HIP events on the kernels' stream), same steps
     h.set_timing(True)

@@ -142,6 +142,22 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used);
  * their bin-major copies. SEPVAD_E_ARG if no forward ran on `stream`. */
 int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream);
 
+/* The forward that sepvad_side_outputs would read: *seq = forwards enqueued so far on `stream` (a per-stream
+ * sequence id), *B / *N = its shape. SEPVAD_E_ARG if no forward ran on `stream`. */
+int32_t sepvad_last_forward(sepvad_handle h, void* stream, int64_t* seq, int32_t* B, int32_t* N);
+
+/* sepvad_side_outputs of ONE forward: fails with SEPVAD_E_ARG (no write) unless forward `seq` of shape (B, N)
+ * (from sepvad_last_forward right after it) is still the last forward on `stream`, so a later forward of another
+ * shape can never be copied into buffers sized for this one (the reference's attributes belong to the forward that
+ * set them, model/model.py:412-429). */
+int32_t sepvad_side_outputs_of(sepvad_handle h, const SepVadOutputs* out, void* stream, int64_t seq, int32_t B,
+                               int32_t N);
+
+/* Synchronises `stream` and frees the per-stream context (workspace, hand-off words, pinned give-up word) the handle
+ * holds for it. Contexts are otherwise kept (at most SEPVAD_MAX_STREAM_CTX = 32 per handle by default, the least
+ * recently used evicted after a sync of its stream). */
+int32_t sepvad_release_stream(sepvad_handle h, void* stream);
+
 /* Block-level parity probe of the fused TCN: while `dump` (device, >= 3 * B * roundup(T, 64) * 256 floats) is
  * set, forwards that run the fused TCN in one launch write dump[0] = TCN.LN output x'_0 (model/model.py:333),
  * dump[1] = block 0's DepthConv1d output (:144) and dump[2] = block 0's TF_Attention output (:207), each

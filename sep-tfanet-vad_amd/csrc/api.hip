@@ -110,6 +110,8 @@ struct StreamCtx {
   unsigned reported = 0;                // last give-up word already returned to the caller
   unsigned tsalt = 0;                   // launch counter (hand-off tag salt)
   int last_B = 0, last_N = 0;           // shape of the last forward on this stream (sepvad_side_outputs)
+  long long seq = 0;                    // forwards enqueued on this stream (side outputs are tied to one)
+  unsigned long long used = 0;          // LRU stamp (context cap, get_ctx)
 };
 
 }  // namespace
@@ -409,7 +411,8 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   const int ln = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
   for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
-    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p);
+    // co-resident workgroups of the persistent TCN kernel that will run (both use one 512-thread workgroup per CU)
+    h->tcn_cap_p[p] = ncu * std::min(tcn_blocks_per_cu(ln, p), tcn_rs_blocks_per_cu(ln, p));
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
   }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
@@ -468,10 +471,23 @@ void free_ctx(StreamCtx* c) {
   delete c;
 }
 
+int env_int(const char* name, int dflt);
 // The context of caller stream `stream` (created on first use; the caller holds h->mu).
 int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
+  static unsigned long long use_clock = 0;
   for (auto& c : h->ctx)
-    if (c->stream == stream) { *out = c.get(); return SEPVAD_OK; }
+    if (c->stream == stream) { c->used = ++use_clock; *out = c.get(); return SEPVAD_OK; }
+  // cap the per-stream contexts (each holds a workspace, hand-off words and pinned memory): evict the least
+  // recently used one after draining its stream (SEPVAD_MAX_STREAM_CTX, default 32)
+  const size_t cap = (size_t)std::max(1, env_int("SEPVAD_MAX_STREAM_CTX", 32));
+  while (h->ctx.size() >= cap) {
+    size_t lru = 0;
+    for (size_t i = 1; i < h->ctx.size(); ++i)
+      if (h->ctx[i]->used < h->ctx[lru]->used) lru = i;
+    HIPCHK(hipStreamSynchronize((hipStream_t)h->ctx[lru]->stream));
+    free_ctx(h->ctx[lru].release());
+    h->ctx.erase(h->ctx.begin() + lru);
+  }
   std::unique_ptr<StreamCtx, void (*)(StreamCtx*)> c(new StreamCtx(), free_ctx);
   c->stream = stream;
   if (h->tcn_cap > 0) {
@@ -488,6 +504,7 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
     const int rc = ws_reserve(c.get(), h->res_B, h->res_N);
     if (rc) return rc;
   }
+  c->used = ++use_clock;
   *out = c.get();
   h->ctx.emplace_back(c.release());
   return SEPVAD_OK;
@@ -943,6 +960,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   stage.next("sepvad::tcn_head");
   const int G = (T + FR - 1) / FR;
   const bool use_fused = fused_ok(h, T);
+  unsigned gsalt_lo = 0, gsalt_n = 0;  // salts of this chunk's k_tcn launches (give-up poisoning, k_istft_pair)
   h->last_fused = use_fused;
   const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
   // the VAD conv1_1 as k_head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
@@ -961,6 +979,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
+    // SEPVAD_TCN_IMPL: 0 (default) = k_tcn (fused.hip), 1 = k_tcn_rs (role-specialised waves, tcn_rs.hip)
+    const bool rs_impl = env_int("SEPVAD_TCN_IMPL", 0) != 0;
+    auto launch_t = [&](const TcnArgs& t, int grid) { return rs_impl ? launch_tcn_rs(t, grid, s) : launch_tcn(t, grid, s); };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     int ngroups = std::min(B, h->tcn_cap_p[h->prec] / G);
@@ -974,6 +995,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
     const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16 * 9;  // wave-0 region + per-wave region
+    gsalt_n = 0;
     for (int u0 = 0; u0 < B; u0 += per_launch) {
       const int Bl = std::min(per_launch, B - u0);
       const int ng = std::min(ngroups, Bl);
@@ -985,6 +1007,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         cx->tsalt = 1;
       }
       ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
+      if (gsalt_n++ == 0) gsalt_lo = cx->tsalt;
       ta.B = Bl;
       ta.S0 = w.S0 + (size_t)u0 * Tp * CH;
       ta.ln = gn_src(w.rec_gate + (size_t)u0 * (Tp / GATE_ROWS) * 2, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
@@ -999,14 +1022,15 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         if (env_int("SEPVAD_TCN_PROBE_WARM", 0)) {  // diagnostics: an unprobed launch first (warm caches)
           TcnArgs tw = ta;
           tw.probe = nullptr;
-          HIPCHK(launch_tcn(tw, ngl * G, s));
+          HIPCHK(launch_t(tw, ngl * G));
           cx->tsalt = (cx->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
           if (cx->tsalt == 0) cx->tsalt = 1;  // (diagnostics: no wrap re-zeroing needed within one forward)
           ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
+          ++gsalt_n;
         }
       }
       if (ev()) return SEPVAD_E_HIP;
-      HIPCHK(launch_tcn(ta, ngl * G, s));
+      HIPCHK(launch_t(ta, ngl * G));
       if (ev()) return SEPVAD_E_HIP;
       if (tr) {
         tr->gemm_ev.push_back((int)h->ev.size() - 2);
@@ -1191,6 +1215,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     is.est_out = out->est ? (float2*)out->est + u2 * NBIN * T : nullptr;
     is.mask_out = out->mask ? out->mask + u2 * NBIN * T : nullptr;
     is.y = out->sep + u2 * N;
+    if (use_fused && gsalt_n > 0) { is.gerr = cx->terr; is.gsalt_lo = gsalt_lo; is.gsalt_n = gsalt_n; }
     TailProbe tp(h, s, "istft");
     is.probe = tp.buf;
     HIPCHK(launch_istft_pair(is, s));
@@ -1212,6 +1237,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   if (rc) return rc;
   cx->last_B = B;
   cx->last_N = N;
+  ++cx->seq;
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   h->ev.clear();
   // diagnostics probe (single chunk only)
@@ -1346,6 +1372,46 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
     if (r && rc == SEPVAD_OK) rc = r;
   }
   return rc;
+}
+
+int32_t sepvad_last_forward(sepvad_handle h, void* stream, int64_t* seq, int32_t* B, int32_t* N) {
+  if (!h || !seq || !B || !N) return fail(SEPVAD_E_ARG, "sepvad_last_forward: null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  for (auto& c : h->ctx)
+    if (c->stream == stream) {
+      *seq = c->seq; *B = c->last_B; *N = c->last_N;
+      return SEPVAD_OK;
+    }
+  return fail(SEPVAD_E_ARG, "sepvad_last_forward: no forward has run on this stream");
+}
+
+int32_t sepvad_release_stream(sepvad_handle h, void* stream) {
+  if (!h) return fail(SEPVAD_E_ARG, "sepvad_release_stream: null handle");
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  for (size_t i = 0; i < h->ctx.size(); ++i)
+    if (h->ctx[i]->stream == stream) {
+      HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+      free_ctx(h->ctx[i].release());
+      h->ctx.erase(h->ctx.begin() + i);
+      return SEPVAD_OK;
+    }
+  return SEPVAD_OK;  // nothing held for this stream
+}
+
+int32_t sepvad_side_outputs_of(sepvad_handle h, const SepVadOutputs* out, void* stream, int64_t seq, int32_t Bx,
+                               int32_t Nx) {
+  if (!h || !out) return fail(SEPVAD_E_ARG, "sepvad_side_outputs_of: null argument");
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    StreamCtx* cx = nullptr;
+    for (auto& c : h->ctx)
+      if (c->stream == stream) cx = c.get();
+    if (!cx || cx->seq != seq || cx->last_B != Bx || cx->last_N != Nx)
+      return fail(SEPVAD_E_ARG, "side outputs: a later forward on the same stream has replaced the workspace of the "
+                                "forward that produced them (read them before the next forward on that stream)");
+  }
+  return sepvad_side_outputs(h, out, stream);
 }
 
 int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream) {

@@ -106,6 +106,11 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   const int T = a.T;
   const int fbeg = f0 - 1;
   const bool vad = a.has_vad != 0;
+  // give-up poisoning (sepvad_internal.h IstftArgs::gerr): NaN outputs for a forward whose fused TCN gave up
+  const unsigned gev = a.gerr ? *a.gerr : 0u;
+  const bool poison =
+      gev != 0u && ((gev >> TCN_EPOCH_BITS) - a.gsalt_lo & ((1u << (32 - TCN_EPOCH_BITS)) - 1u)) < a.gsalt_n;
+  const float qnan = __builtin_nanf("");
   // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
   unsigned long long* const pr = a.probe ? a.probe + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int k) {
@@ -226,7 +231,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
         for (int k = 0; k < 3; ++k) z = fmaf(a.w2[o * 3 + k], yn[sp][o][qq + k], z);
       const float p = sigmoid_f(z);
       vadv[sp][qq] = (f >= 0 && f < T) ? p : 0.f;
-      if (!a.kw_enabled && f >= f0 && f < f0 + IP_OWN && f < T) a.vad_out[((size_t)b * 2 + sp) * T + f] = p;
+      if (!a.kw_enabled && f >= f0 && f < f0 + IP_OWN && f < T) a.vad_out[((size_t)b * 2 + sp) * T + f] = poison ? qnan : p;
     }
     lds_sync();
     if (tid < 2 * IP_FR) {
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
         if (f == 0 || f == T - 1) smv = thr(f);
         if (a.filt) gg = smv;
         if (f >= f0 && f < f0 + IP_OWN)
-          a.vad_out[((size_t)b * 2 + sp) * T + f] = a.ret_smooth ? smv : vadv[sp][f - (fbeg - 2)];
+          a.vad_out[((size_t)b * 2 + sp) * T + f] = poison ? qnan : (a.ret_smooth ? smv : vadv[sp][f - (fbeg - 2)]);
       }
       gain[sp][fi] = gg;
     }
@@ -267,9 +272,10 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
         if (a.est_out) {
           const float2 e = spec[sp][fo + 1][k];
           const float gg = gain[sp][fo + 1];
-          st_out(a.est_out + o, make_float2(gg * e.x, gg * e.y));
+          st_out(a.est_out + o, poison ? make_float2(qnan, qnan) : make_float2(gg * e.x, gg * e.y));
         }
-        if (a.mask_out) st_out(a.mask_out + o, sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]));
+        if (a.mask_out)
+          st_out(a.mask_out + o, poison ? qnan : sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]));
       }
     }
     lds_sync();  // the transforms below overwrite the rows
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
       float num = 0.f;
       if (j < T) num += reinterpret_cast<const float*>(spec[sp][j - fbeg])[q];  // frame j, first half
       num += reinterpret_cast<const float*>(spec[sp][j - 1 - fbeg])[q + HOP];    // frame j-1, second half
-      st_out(yb + n, num * (j < T ? inv_mid : inv_last));
+      st_out(yb + n, poison ? qnan : num * (j < T ? inv_mid : inv_last));
     }
   }
   stamp(5);

@@ -207,6 +207,12 @@ struct IstftArgs {
   float* mask_out;       // nullable [BS][NBIN][T]
   float* y;              // [BS][N]
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
+  // give-up poisoning (fused TCN): when the stream context's give-up word (tag0 of a k_tcn launch whose bounded
+  // hand-off wait gave up) names one of this forward's launches (salts gsalt_lo .. gsalt_lo + gsalt_n - 1, modulo the
+  // salt width), every output of the launch (sep, vad, est, mask) is written as NaN: no invalid output is returned
+  // as a valid one, stream-ordered, no host synchronisation. gerr nullable (no fused TCN in this forward).
+  const unsigned* gerr;
+  unsigned gsalt_lo, gsalt_n;
 };
 
 // streaming wrapper (stream.hip)
@@ -272,7 +278,7 @@ constexpr int FR = 32;          // frames per workgroup
 constexpr int FG_MAX = 32;      // workgroups per utterance (T <= 1024: 16.4 s at 16 kHz in one fused forward)
 constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
 constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
-constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
+constexpr int NGR = 2368;       // 8-byte {tag, value} hand-off words per slot (k_tcn: >= 4 + 8 * 256; k_tcn_rs: 2367)
 constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
 constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine
@@ -313,6 +319,10 @@ struct TcnArgs {
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
+// The same TCN as ONE persistent launch with role-specialised waves (tcn_rs.hip: matrix waves run the GEMMs,
+// vector waves the depthwise conv, polls and gates); same arguments, outputs and hand-off buffer.
+hipError_t launch_tcn_rs(const TcnArgs& a, int grid, hipStream_t s);
+int tcn_rs_blocks_per_cu(int ln_mode, int prec);
 // Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
 // for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
 struct HeadArgs {

@@ -1,0 +1,187 @@
+// Device helpers shared by the two persistent TCN kernels (fused.hip k_tcn, tcn_rs.hip k_tcn_rs):
+// MFMA operand types, wave-uniform buffer descriptors, the tagged 8-byte hand-off words ("data is its own
+// flag", cdna_hip_programming.md Guideline 16 R2) with bounded polls, DPP lane reductions and the fp16 hi/lo
+// operand split.
+#pragma once
+#include "device_common.h"
+
+namespace sepvad {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+// Wave-uniform copies (readfirstlane) of values loaded from the block-parameter table: the compiler cannot
+// prove those loads uniform, and a buffer descriptor in VGPRs becomes a waterfall loop per access.
+template <typename Tp>
+__device__ __forceinline__ Tp* uni(Tp* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (Tp*)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float unif(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+}
+// Buffer descriptor over a wave-uniform base. The base goes through readfirstlane: under SGPR pressure
+// hipcc keeps uniform pointers in VGPRs, and a descriptor it cannot prove uniform turns every buffer
+// access into a waterfall loop (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uni(p)), (short)0, 0x7fffffff, 0x00020000);
+}
+typedef unsigned long long u64;
+// ---- hand-off words: 8-byte {tag, value} granules (the data is its own flag) ----
+// Same-XCD groups: plain stores keep the words in the XCD's shared L2; otherwise agent-scope (sc1)
+// write-through stores. Consumers always load with agent-scope relaxed atomics (sc1: L1 bypass).
+__device__ __forceinline__ void gput(u64* p, unsigned tag, unsigned v, bool l2) {
+  const u64 w = ((u64)tag << 32) | v;
+  if (l2) __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gputf(u64* p, unsigned tag, float v, bool l2) {
+  gput(p, tag, __builtin_bit_cast(unsigned, v), l2);
+}
+__device__ __forceinline__ void gputd(u64* p, unsigned tag, double v, bool l2) {  // two consecutive words
+  const u64 b = __builtin_bit_cast(u64, v);
+  gput(p, tag, (unsigned)b, l2);
+  gput(p + 1, tag, (unsigned)(b >> 32), l2);
+}
+__device__ __forceinline__ double dword2(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
+}
+// Poll the N words p[k] (nullptr = none) until every tag equals `tag`; values into v[k]. All loads of a
+// pass are in flight together. Bounded: gives up after a.spin_limit passes, or as soon as another
+// workgroup of this launch gave up (the device word then holds this launch's tag0), and records the give-up
+// in the device word and in its host-mapped copy; the launch then runs to completion with invalid outputs
+// instead of hanging, and the host reports it (sepvad_forward / sepvad_fused_status). Words of earlier
+// launches' give-ups hold other tags, so a give-up never leaks into a later launch.
+__device__ __forceinline__ void giveup(const TcnArgs& a) {
+  __hip_atomic_store(a.err, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.herr != nullptr) __hip_atomic_store(a.herr, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <int N>
+__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], const TcnArgs& a) {
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (p[k] != nullptr) {
+        const u64 x = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = (unsigned)x;
+        ok = ok && (unsigned)(x >> 32) == tag;
+      }
+    }
+    if (ok) return;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0 &&
+        (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
+      giveup(a);
+      return;
+    }
+  }
+}
+// gpoll with a tag per word (one round over words of different hand-offs)
+template <int N>
+__device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned (&tag)[N], unsigned (&v)[N],
+                                       const TcnArgs& a) {
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (p[k] != nullptr) {
+        const u64 x = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = (unsigned)x;
+        ok = ok && (unsigned)(x >> 32) == tag[k];
+      }
+    }
+    if (ok) return;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0 &&
+        (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
+      giveup(a);
+      return;
+    }
+  }
+}
+
+// One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
+// bf16 bits (BF16, round to nearest even) in the hi plane.
+template <int PRE>
+__device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, int idx, float v) {
+  if constexpr (PRE == PREC_F16X3) {
+    const _Float16 h = (_Float16)v;
+    hi[idx] = h;
+    lo[idx] = (_Float16)(v - (float)h);
+  } else if constexpr (PRE == PREC_F16) {
+    hi[idx] = (_Float16)v;
+  } else {
+    reinterpret_cast<__bf16*>(hi)[idx] = (__bf16)v;
+  }
+}
+
+// two adjacent values (idx even): one 32-bit LDS store per plane
+template <int PRE>
+__device__ __forceinline__ void split_store2(_Float16* hi, _Float16* lo, int idx, float v0, float v1) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  if constexpr (PRE == PREC_F16X3) {
+    const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+    *reinterpret_cast<f16x2*>(hi + idx) = f16x2{h0, h1};
+    *reinterpret_cast<f16x2*>(lo + idx) = f16x2{(_Float16)(v0 - (float)h0), (_Float16)(v1 - (float)h1)};
+  } else if constexpr (PRE == PREC_F16) {
+    *reinterpret_cast<f16x2*>(hi + idx) = f16x2{(_Float16)v0, (_Float16)v1};
+  } else {
+    *reinterpret_cast<bf16x2*>(hi + idx) = bf16x2{(__bf16)v0, (__bf16)v1};
+  }
+}
+
+// DPP lane reductions (no LDS round trip, fixed order => deterministic). update_dpp with old = 0:
+// lanes whose DPP source is out of range add 0.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// quad_perm [1,0,3,2], [2,3,0,1], row_shr:4, row_shr:8, row_bcast:15 => lane 31 holds the sum of lanes
+// 0..31 and lane 63 the sum of lanes 32..63.
+__device__ __forceinline__ float half_total(float v) {
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  v += dpp_f<0x142>(v);
+  return v;
+}
+// Sum over the 64 lanes (+ row_bcast:31), returned wave-uniform (lane 63).
+__device__ __forceinline__ float wave_total(float v) {
+  v = half_total(v);
+  v += dpp_f<0x143>(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const u64 b = __builtin_bit_cast(u64, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
+}
+// This thread's workgroup-relative id, recomputed where it is needed: the wave index from a wave-uniform
+// SGPR, the lane from v_mbcnt (volatile asm: never hoisted). Values derived from threadIdx.x before the
+// utterance loop stay live across all of it; at 256 VGPRs hipcc spills them to scratch, and the first
+// reloads of a launch (behind the scratch spill stores, vmcnt(0)) cost ~15 us of cold-start latency.
+__device__ __forceinline__ int fresh_tid(int wave_s) {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return wave_s * 64 + l;
+}
+
+// The kernel arguments re-read from the kernarg segment (scalar loads through an opaque pointer) where
+// the prologue uses them: pointers held in registers across the utterance loop end up in VGPRs and are
+// spilled to scratch at this register pressure.
+typedef const __attribute__((address_space(4))) TcnArgs* KArgs;
+__device__ __forceinline__ KArgs kargs() {
+  KArgs p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+}  // namespace sepvad

@@ -198,10 +198,11 @@ class SeparationModel(nn.Module):
             src = self.__dict__.get("_side_src")
             if src is None:
                 raise AttributeError(f"'SeparationModel' has no attribute '{name}' before the first forward")
-            h, stream, B, T = src
-            # masks_b and mask_per_speaker come from one kernel: materialise both together
+            h, stream, B, T, N, seq = src
+            # masks_b and mask_per_speaker come from one kernel: materialise both together; the library checks
+            # that this forward (seq, B, N) is still the stream's last one (raises otherwise, writes nothing)
             want = (name,) if name == "spectrum" else tuple(n for n in ("masks_b", "mask_per_speaker") if n not in cache)
-            cache.update(h.side_outputs(stream, B, T, want))
+            cache.update(h.side_outputs(stream, B, T, want, seq=seq, N=N))
         return cache[name]
 
     def _side_set(self, name, value):
@@ -226,7 +227,7 @@ class SeparationModel(nn.Module):
                 out = h.forward(x, inference_kw if inference_kw else None)
         else:
             out = h.forward(x, inference_kw if inference_kw else None)
-        self.__dict__["_side_src"] = (h, out["stream"], out["B"], out["T"])
+        self.__dict__["_side_src"] = (h, out["stream"], out["B"], out["T"], out["N"], out["seq"])
         self.__dict__["_side_cache"] = {}
         self.estimated_stfts = out["est"]
         return out["sep"], out["vad"], out["est"]

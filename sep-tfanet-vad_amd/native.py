@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
     "sepvad_forward_windows", "sepvad_pit_l1_sums", "sepvad_pit_l1_choose",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
+    "sepvad_last_forward", "sepvad_side_outputs_of", "sepvad_release_stream",
     "sepvad_stft", "sepvad_istft",
     "sepvad_pit_l1", "sepvad_stream_append",
     "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_vad_accuracy",
@@ -97,6 +98,12 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_set_tcn_dump.argtypes = [P, P]
     lib.sepvad_side_outputs.restype = i32
     lib.sepvad_side_outputs.argtypes = [P, ctypes.POINTER(SepVadOutputs), P]
+    lib.sepvad_last_forward.restype = i32
+    lib.sepvad_last_forward.argtypes = [P, P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    lib.sepvad_side_outputs_of.restype = i32
+    lib.sepvad_side_outputs_of.argtypes = [P, ctypes.POINTER(SepVadOutputs), P, ctypes.c_int64, i32, i32]
+    lib.sepvad_release_stream.restype = i32
+    lib.sepvad_release_stream.argtypes = [P, P]
     lib.sepvad_stft.restype = i32
     lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft.restype = i32
@@ -282,7 +289,11 @@ class Handle:
             vad_ret = vad.view(B, S, 1, T)  # model/model.py:456-457
         else:
             vad_ret = vad
-        res = dict(sep=sep, vad=vad_ret, est=est, stream=stream.value or 0, B=B, T=T)
+        seq = ctypes.c_int64()
+        lb, ln = ctypes.c_int32(), ctypes.c_int32()
+        _check(self._lib.sepvad_last_forward(self._h, stream, ctypes.byref(seq), ctypes.byref(lb), ctypes.byref(ln)),
+               "sepvad_last_forward")
+        res = dict(sep=sep, vad=vad_ret, est=est, stream=stream.value or 0, B=B, T=T, N=N, seq=seq.value)
         if return_aux:
             res.update(spectrum=spectrum, masks_b=masks_b, mask_per_speaker=mask)
         return res
@@ -308,17 +319,19 @@ class Handle:
             self.fused_status()
         return sep
 
-    def side_outputs(self, stream: int, B: int, T: int, want=("spectrum", "masks_b", "mask_per_speaker")):
-        """The side attributes of the last forward on `stream` (sepvad_side_outputs), materialised now on that
-        stream: dict with the requested subset of spectrum [B,257,T], masks_b [B,514,T] and
-        mask_per_speaker [B,2,257,T]."""
+    def side_outputs(self, stream: int, B: int, T: int, want=("spectrum", "masks_b", "mask_per_speaker"),
+                     seq: int | None = None, N: int | None = None):
+        """The side attributes of forward `seq` (shape B x N) on `stream` (sepvad_side_outputs_of), materialised
+        now on that stream: dict with the requested subset of spectrum [B,257,T], masks_b [B,514,T] and
+        mask_per_speaker [B,2,257,T]. Raises RuntimeError if a later forward on that stream replaced its workspace
+        (nothing is written then). Without seq: the last forward on the stream (sepvad_side_outputs).
+        The tensors are safe to use on the caller's current stream (it waits for the copies)."""
         F = self.cfg["n_fftBins"] // 2 + 1
         S = self.cfg["num_spk"]
         cur = torch.cuda.current_stream(self.device)
-        ctx = torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)) if cur.cuda_stream != stream \
-            else torch.cuda.stream(cur)
+        fwd = torch.cuda.ExternalStream(stream, device=self.device) if cur.cuda_stream != stream else cur
         res = {}
-        with ctx:
+        with torch.cuda.stream(fwd):
             dev = self.device
             if "spectrum" in want:
                 res["spectrum"] = torch.empty(B, F, T, device=dev, dtype=torch.float32)
@@ -328,9 +341,23 @@ class Handle:
                 res["mask_per_speaker"] = torch.empty(B, S, F, T, device=dev, dtype=torch.float32)
             outs = SepVadOutputs(0, 0, 0, _ptr(res.get("spectrum")).value, _ptr(res.get("masks_b")).value,
                                  _ptr(res.get("mask_per_speaker")).value)
-            _check(self._lib.sepvad_side_outputs(self._h, ctypes.byref(outs), ctypes.c_void_p(stream)),
-                   "sepvad_side_outputs")
+            if seq is None:
+                rc = self._lib.sepvad_side_outputs(self._h, ctypes.byref(outs), ctypes.c_void_p(stream))
+            else:
+                rc = self._lib.sepvad_side_outputs_of(self._h, ctypes.byref(outs), ctypes.c_void_p(stream), seq, B, N)
+            _check(rc, "sepvad_side_outputs")
+        if fwd is not cur:  # the caller's stream waits for the copies; the allocator keeps the blocks until then
+            cur.wait_stream(fwd)
+            for t in res.values():
+                t.record_stream(cur)
         return res
+
+    def release_stream(self, stream: int | None = None):
+        """Free the per-stream context (workspace, hand-off words) the handle keeps for `stream` (default: the
+        current stream) after synchronising it (sepvad_release_stream)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        _check(self._lib.sepvad_release_stream(self._h, ctypes.c_void_p(stream)), "sepvad_release_stream")
 
     def tcn_dump(self, x: torch.Tensor):
         """Block-level parity probe (sepvad_set_tcn_dump): one forward of x with the fused TCN, returning

@@ -9,7 +9,8 @@ device:
 
 * all windows of all streams run as ONE forward (``sepvad_forward_windows``): window k of stream b is read at
   x + b * row + k * hop, no gather copy (``get_truncated_signal``, :39-41); only the PIT-L1 + append chain
-  is sequential over windows;
+  is sequential over windows; recordings longer than ``max_window_utts`` window-utterances run in window-major
+  chunks of forwards (bounded workspace, same results);
 * the stitched signal is one preallocated ``[B, 2, n_windows * hop]`` buffer; the reorder + append
   of each hop is one ``sepvad_stream_append`` launch (``reorder_source_mse`` + ``update_online_signal``,
   :28-37, :93-94); the permutation comes from ``sepvad_pit_l1`` and never leaves the device;
@@ -49,6 +50,9 @@ class OnlineSaving:
         self.num_save_samples = 30
         self.similarity = False
         self.one_forward = True  # all windows in one forward when possible (False: the reference's window loop)
+        # window-utterances per forward_windows call: long recordings run in window-major chunks, so the
+        # workspace (~2.5 MB per window-utterance at T = 188) stays bounded (cfg 3: 1 792 in one call)
+        self.max_window_utts = 2048
         if criterion_similarity is not None:
             self.similarity = True
             self.criterion_similarity = criterion_similarity
@@ -152,11 +156,16 @@ class OnlineSaving:
             x = full_signal_mix.to(torch.float32)
             if x.stride(-1) != 1:
                 x = x.contiguous()
-            with torch.no_grad():
-                sep_w = self.model.native_handle(dev).forward_windows(x, n_win, hop, win, inference_kw)
+            wchunk = max(1, int(self.max_window_utts) // max(1, B))
+            k_base, sep_w = 0, None
         while self.indx <= max_indx:
             if batched:
-                pred_separation = sep_w[self.indx]
+                k = self.indx
+                if sep_w is None or k >= k_base + sep_w.shape[0]:  # next window-major chunk, one forward
+                    k_base, n = k, min(wchunk, n_win - k)
+                    with torch.no_grad():
+                        sep_w = self.model.native_handle(dev).forward_windows(x[:, k * hop:], n, hop, win, inference_kw)
+                pred_separation = sep_w[k - k_base]
             else:
                 truncated_signal_mix = self.get_truncated_signal(full_signal_mix)
                 with torch.no_grad():

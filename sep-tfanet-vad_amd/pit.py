@@ -27,10 +27,12 @@ _scratch = {}
 def _scratch_for(device):
     """Scratch of the current stream on `device` (one per stream: concurrent streams never share it)."""
     key = (device, torch.cuda.current_stream(device).cuda_stream)
-    buf = _scratch.get(key)
+    buf = _scratch.pop(key, None)
     if buf is None:
         buf = torch.empty(PIT_SCRATCH_BYTES // 8, dtype=torch.float64, device=device)
-        _scratch[key] = buf
+        while len(_scratch) >= 32:  # bounded: drop the least recently used stream's scratch (its blocks return
+            _scratch.pop(next(iter(_scratch)))  # to that stream's allocator pool, reused only in its order)
+    _scratch[key] = buf  # most recently used last
     return buf
 
 
@@ -84,7 +86,12 @@ def pit_l1_sharded(est: torch.Tensor, ref: torch.Tensor, total_rows: int, group=
     rc = lib.sepvad_pit_l1_sums(_native._ptr(est), eld, _native._ptr(ref), rld, B, L, _native._ptr(_scratch_for(dev)),
                                 _native._ptr(buf), _stream(dev))
     _native._check(rc, "sepvad_pit_l1_sums")
-    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    if dist.get_backend(group) == "gloo":  # (tests on a shared GPU: gloo reduces host tensors)
+        hb = buf.cpu()
+        dist.all_reduce(hb, op=dist.ReduceOp.SUM, group=group)
+        buf.copy_(hb)
+    else:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     count = float(total_rows) * float(L)
     perm = torch.empty(B, 2, dtype=torch.int64, device=dev)
     loss = torch.empty((), dtype=torch.float32, device=dev)

@@ -51,3 +51,43 @@ def test_bench_rccl_path_one_json_line():
     assert len(lines) == 1, p.stdout[:2000]
     d = json.loads(lines[0])
     assert KEYS <= d.keys() and d["n_gpus"] == 1 and d["value"] > 0
+
+
+def _one_json(p):
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[:2000]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_through_the_launcher():
+    """bench.py --gpus 2 outside torchrun: launch_ranks starts a child torch.distributed.run with two ranks (here both
+    on cuda:0 over gloo, SEPVAD_BENCH_SHARE_GPU=1: RCCL needs a GPU per rank); exactly one JSON line from rank 0 with
+    the whole-job numbers. Two persistent k_tcn grids share the chip and both finish (no cooperative launch)."""
+    env = dict(os.environ, SEPVAD_BENCH_SHARE_GPU="1")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                       cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
+    d = _one_json(p)
+    assert KEYS <= d.keys()
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 128 and d["value"] > 0
+
+
+def test_bench_stream_two_ranks_equal_one_rank(tmp_path):
+    """cfg 3 sharded over two ranks (256 streams each, the PIT-L1 sums all-reduced: model/pit_wrapper.py:172-177 is
+    batch-global) equals one rank running all 512 streams, bitwise (stream inputs are seeded per stream)."""
+    env2 = dict(os.environ, SEPVAD_BENCH_SHARE_GPU="1", SEPVAD_BENCH_DUMP=str(tmp_path / "w2"))
+    p2 = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--workload", "stream", "--steps", "1", "--warmup",
+                         "0", "--no-cpu-baseline"], cwd=REPO, capture_output=True, text=True, timeout=280, env=env2)
+    d2 = _one_json(p2)
+    assert d2["n_gpus"] == 2 and d2["config"]["global_batch"] == 512
+    env1 = dict(os.environ, SEPVAD_BENCH_DUMP=str(tmp_path / "w1"))
+    p1 = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--workload", "stream", "--batch", "512",
+                         "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], cwd=REPO, capture_output=True, text=True,
+                        timeout=280, env=env1)
+    _one_json(p1)
+    import numpy as np
+    a = np.concatenate([np.load(str(tmp_path / "w2.rank0.npy")), np.load(str(tmp_path / "w2.rank1.npy"))])
+    b = np.load(str(tmp_path / "w1.rank0.npy"))
+    assert a.shape == b.shape == (512, 2, 7 * 2560)
+    assert np.isfinite(a).all()
+    assert np.array_equal(a, b)

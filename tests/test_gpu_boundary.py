@@ -3,8 +3,12 @@
 * concurrent forwards on different streams of ONE handle are allowed: each caller stream gets its own
   workspace, hand-off words and give-up words, so two streams running at once give the same bits as a
   serial run;
-* a fused-TCN hand-off give-up never passes as success: it is reported by the next forward on the same
-  stream (or by fused_status / SEPVAD_CHECK=1), is not sticky, and the forward after it is valid again;
+* a fused-TCN hand-off give-up never passes as success: the forward that gave up writes NaN outputs (stream-
+  ordered, no host sync), the next forward on the same stream reports it (or fused_status / SEPVAD_CHECK=1), it
+  is not sticky, and the forward after it is valid again;
+* side attributes belong to the forward that produced them: reading them after a later forward on the same stream
+  raises instead of copying another forward's (differently shaped) workspace; they are safe to read on another
+  stream; a stream's context can be released;
 * a batch split over several persistent launches (launch salts, epoch counters) is bitwise equal to one;
 * the fp16 split of the GEMM operands keeps fp32-equivalent accuracy when weights or inputs are scaled
   by 1e-3 or 1e3 (static power-of-two range scales, api.hip range_exp).
@@ -86,6 +90,73 @@ def test_giveup_is_reported_once_and_not_sticky(net):
     assert h.fused_status()  # not sticky
     out = h.forward(x)
     assert np.abs(out["sep"].cpu().numpy() - g["sep"]).max() <= SEP_TOL
+
+
+def test_giveup_poisons_the_same_forward(net):
+    """The forward whose k_tcn hand-off gave up returns NaN in sep, vad and est (k_istft_pair reads the give-up word,
+    stream-ordered): no invalid output passes as a valid one even for a caller's last or only forward."""
+    g = load_golden("with_vad", "small")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    h = net.native_handle(DEV)
+    good = h.forward(x)
+    assert not torch.isnan(good["sep"]).any()
+    os.environ["SEPVAD_TCN_FORCE_GIVEUP"] = "1"
+    try:
+        bad = h.forward(x)
+    finally:
+        del os.environ["SEPVAD_TCN_FORCE_GIVEUP"]
+    torch.cuda.synchronize()
+    assert torch.isnan(bad["sep"]).all()
+    assert torch.isnan(bad["vad"]).all()
+    assert torch.isnan(torch.view_as_real(bad["est"])).all()
+    with pytest.raises(RuntimeError, match="gave up"):
+        h.forward(x)
+    out = h.forward(x)
+    assert h.fused_status()
+    assert not torch.isnan(out["sep"]).any()
+    assert np.abs(out["sep"].cpu().numpy() - g["sep"]).max() <= SEP_TOL
+
+
+def test_stale_side_attributes_raise(net):
+    """net(xa); a later forward of another shape on the same stream (Handle.forward, or the streaming wrapper's
+    window forward); reading net.spectrum must raise, never copy that forward's workspace into xa-sized tensors."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    xa = torch.from_numpy(synth.make_batch(3, 20000, 41)[0]).to(DEV)
+    xb = torch.from_numpy(synth.make_batch(9, 32000, 42)[0]).to(DEV)
+    with torch.no_grad():
+        net(xa)
+    h.forward(xb)
+    with pytest.raises(RuntimeError, match="later forward"):
+        _ = net.spectrum
+    with pytest.raises(RuntimeError, match="later forward"):
+        _ = net.mask_per_speaker
+    eager = h.forward(xa, return_aux=True)
+    with torch.no_grad():
+        net(xa)
+    assert torch.equal(net.spectrum, eager["spectrum"])
+    assert torch.equal(net.masks_b, eager["masks_b"])
+
+
+def test_side_attributes_read_on_another_stream(net):
+    """A forward on a side stream, its side attributes read on the default stream: the reader's stream waits for
+    the copies (wait_stream / record_stream), values equal the eager ones."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(4, 24000, 43)[0]).to(DEV)
+    eager = h.forward(x, return_aux=True)
+    torch.cuda.synchronize()
+    s1 = torch.cuda.Stream()
+    with torch.cuda.stream(s1), torch.no_grad():
+        net(x)
+    m = net.mask_per_speaker.clone()  # default stream
+    assert torch.equal(m, eager["mask_per_speaker"])
+    assert torch.equal(net.spectrum, eager["spectrum"])
+    h.release_stream(s1.cuda_stream)  # the side stream's context freed after a sync; a new forward re-creates it
+    with torch.cuda.stream(s1), torch.no_grad():
+        r = h.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(r["sep"], eager["sep"])
 
 
 def test_several_launches_per_forward_are_bitwise_identical(net):

@@ -117,6 +117,44 @@ def test_one_forward_equals_window_loop(net, tmp_path):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_chunked_windows_equal_one_forward(net, tmp_path):
+    """Recordings longer than max_window_utts window-utterances run as several window-major forward_windows calls:
+    bitwise equal to one call (bounded workspace)."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(5, 64000, 4101)[0]).to(DEV)
+    outs = []
+    for cap in (10 ** 6, 10, 5):  # one call; 2 windows per call; 1 window per call
+        ons = pkg.OnlineSaving(net, str(tmp_path), _criterion())
+        ons.save_sec = 0.16
+        ons.max_window_utts = cap
+        ons.calc_online(x, "s", 10 ** 6, dict(pkg.INFERENCE_KW_DEFAULTS))
+        outs.append(ons.online_signal.clone())
+    assert outs[0].shape == (5, 2, 7 * 2560)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+def test_cfg3_full_size_one_forward_equals_window_loop(net, tmp_path):
+    """BASELINE cfg 3 at its real size: 256 streams x 64 000 samples (4 s), 160 ms hop = 7 windows of 48 000 samples;
+    the one-forward path (1 792 windows of T = 188 in one sepvad_forward_windows) equals the reference's window
+    loop (one forward of 256 per window, model/online_class_unknown_targets.py:72-105) bitwise, on the fused TCN."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(256, 64000, 4102)[0]).to(DEV)
+    h = net.native_handle(DEV)
+    outs = []
+    for one in (True, False):
+        ons = pkg.OnlineSaving(net, str(tmp_path), _criterion())
+        ons.save_sec = 0.16
+        ons.one_forward = one
+        ons.calc_online(x, "s", 10 ** 6, dict(pkg.INFERENCE_KW_DEFAULTS))
+        assert h.fused_status()
+        outs.append(ons.online_signal.clone())
+    assert outs[0].shape == (256, 2, 7 * 2560)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_pit_sums_decompose_over_shards():
     """What a sharded stream batch does per window (pit_l1_sharded): the 4 pairwise L1 sums of each shard,
     summed (the all-reduce), then the batch-global choice == the unsharded sepvad_pit_l1 (same permutation,
