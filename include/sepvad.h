@@ -158,6 +158,18 @@ int32_t sepvad_side_outputs_of(sepvad_handle h, const SepVadOutputs* out, void* 
  * recently used evicted after a sync of its stream). */
 int32_t sepvad_release_stream(sepvad_handle h, void* stream);
 
+/* Kernel-level test entries of the forward's own front and back end (the fused schedule's k_stft_gate and
+ * k_istft_pair), in the frame-major layouts the forward's workspace holds (Tp = roundup(T, 64), T = 1 + N / 256):
+ * sepvad_stft_gate_test: X_fm [B][Tp][257] complex (DC zeroed) and db_fm [B][Tp][260] = 10 log10(clamp(|X|^2, 1e-10))
+ * of x [B][N] (model/model.py:16-25,408-412; the activity gate's outputs go to the stream's workspace).
+ * sepvad_istft_pair_test: est[b][s] = X_fm[b] * sigmoid(masks_fm[b][:, 257 s + k]) and y[b][s] = torch.istft(est,
+ * center=True, length=N) (model/model.py:429-460, no VAD gain), y [B][2][N], est (nullable) [B][2][257][T] complex,
+ * masks_fm [B][Tp][576]. Tests only. */
+int32_t sepvad_stft_gate_test(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X_fm, float* db_fm,
+                              void* stream);
+int32_t sepvad_istft_pair_test(sepvad_handle h, const void* X_fm, const float* masks_fm, int32_t B, int32_t N, float* y,
+                               void* est, void* stream);
+
 /* Block-level parity probe of the fused TCN: while `dump` (device, >= 3 * B * roundup(T, 64) * 256 floats) is
  * set, forwards that run the fused TCN in one launch write dump[0] = TCN.LN output x'_0 (model/model.py:333),
  * dump[1] = block 0's DepthConv1d output (:144) and dump[2] = block 0's TF_Attention output (:207), each

@@ -1441,6 +1441,45 @@ int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* str
   return SEPVAD_OK;
 }
 
+int32_t sepvad_stft_gate_test(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X_fm, float* db_fm,
+                              void* stream) {
+  if (!h || !x || !X_fm || !db_fm || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_stft_gate_test: bad arguments");
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  StreamCtx* cx = nullptr;
+  int rc = get_ctx(h, stream, &cx);
+  if (rc) return rc;
+  rc = ws_reserve(cx, B, N);  // S0 and the TCN.LN records land in this stream's workspace
+  if (rc) return rc;
+  const int T = 1 + N / HOP, Tp = round_up(T, TILE);
+  const Workspace w = ws_view(cx->ws, 0, Tp);
+  StftArgs sa{};
+  sa.B = B; sa.N = N; sa.ldx = N; sa.T = T; sa.Tp = Tp; sa.x = x; sa.tw = (const float2*)h->P(h->tw);
+  sa.nstr = B; sa.hopw = 0;
+  sa.window = h->P(h->win_out);
+  sa.window_db = h->same_stft_window ? sa.window : h->P(h->win_in);
+  sa.X = (float2*)X_fm; sa.specdb = db_fm; sa.db_out = 1;
+  sa.activity = h->cfg.activity_input; sa.gate_w = h->P(h->gate);
+  sa.S0 = w.S0; sa.gate_rec = w.rec_gate;
+  HIPCHK(launch_stft_gate(sa, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_istft_pair_test(sepvad_handle h, const void* X_fm, const float* masks_fm, int32_t B, int32_t N, float* y,
+                               void* est, void* stream) {
+  if (!h || !X_fm || !masks_fm || !y || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_istft_pair_test: bad arguments");
+  DeviceGuard dg(h->device);
+  const int T = 1 + N / HOP, Tp = round_up(T, TILE);
+  IstftArgs is{};
+  is.BS = B * 2; is.S = 2; is.N = N; is.T = T; is.Tp = Tp; is.est_mode = 1;
+  is.X = (const float2*)X_fm; is.masks = masks_fm;
+  is.window = h->P(h->win_inv); is.tw = (const float2*)h->P(h->tw);
+  is.has_vad = 0;
+  is.est_out = (float2*)est; is.y = y;
+  HIPCHK(launch_istft_pair(is, (hipStream_t)stream));
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_stft(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X, float* spec, void* stream) {
   if (!h || !x || B < 1 || N <= HOP) return fail(SEPVAD_E_ARG, "sepvad_stft: bad arguments");
   DeviceGuard dg(h->device);

@@ -64,6 +64,12 @@ namespace sepvad {
 #ifndef TCN_SUB
 #define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)
 #endif
+#ifndef TCN_DWP
+#define TCN_DWP 0    // depthwise conv in packed fp32 over channel pairs (1) or one channel per thread, scalar (0)
+#endif
+#ifndef TCN_PKE
+#define TCN_PKE 0    // elementwise phases (epilogue, gates, moments, x' update) in packed fp32 over row pairs (1)
+#endif
 #ifndef TCN_EPI
 #define TCN_EPI 1    // conv1d epilogue parameters from global into registers: no barrier before the epilogue
 #endif
@@ -96,6 +102,8 @@ struct TcnSmem {
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
+static_assert(offsetof(TcnSmem, at) % 8 == 0 && offsetof(TcnSmem, H) % 8 == 0 && offsetof(TcnSmem, prm) % 16 == 0,
+              "packed (8-byte) reads of at / H / the parameter blob");
 
 // granule word layout of one slot
 constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq hi}; P4: 11 doubles as 22 words
@@ -440,6 +448,32 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         u64* s1 = slot(g, e1);
         float st[2] = {0.f, 0.f};
+#if TCN_PKE
+        // packed fp32 over row pairs (r, r+1) = frames (tl, tl+1)
+        {
+          const float a1m1 = a1 - 1.f;
+          f32x2 s0 = {0.f, 0.f}, q0 = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int tl = trow(r);
+            const f32x2 z = __builtin_elementwise_fma(f32x2{acc[r], acc[r + 1]}, f32x2{ws, ws}, f32x2{bias, bias});
+            const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+            const f32x2 v = prelu2(z, a1m1) * vm;
+            sm.H[(tl + 4) * CH + m] = v.x;
+            sm.H[(tl + 5) * CH + m] = v.y;
+            s0 += v;
+            q0 = __builtin_elementwise_fma(v, v, q0);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const float ve = e ? v.y : v.x;
+              if (r + e < 4 && hl == 0 && tl + e < dil) gputf(s1 + GW_TOP + (tl + e) * CH + m, tag1, ve, l2);
+              if (r + e >= 12 && hl == 1 && tl + e >= FR - dil) gputf(s1 + GW_BOT + (tl + e - (FR - dil)) * CH + m, tag1, ve, l2);
+            }
+          }
+          st[0] = s0.x + s0.y;
+          st[1] = q0.x + q0.y;
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int tl = trow(r);
@@ -450,6 +484,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           if (r < 4 && hl == 0 && tl < dil) gputf(s1 + GW_TOP + tl * CH + m, tag1, v, l2);
           if (r >= 12 && hl == 1 && tl >= FR - dil) gputf(s1 + GW_BOT + (tl - (FR - dil)) * CH + m, tag1, v, l2);
         }
+#endif
         if (TCN_SUB == 2) TPROBE(13);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H complete
         if (TCN_SUB == 2) TPROBE(14);
@@ -509,10 +544,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const float a2 = pm[PB_A2];
         // GN1 affine of this thread's channel, computed in-thread from the members' sums (member order,
         // as gn_affine: no LDS round trip, no barrier)
-        float sc, sh;
+        float mu, rs;
         {
 #if TCN_GNW
-          float mu, rs;
           if (G <= FG_WAVE) {
             mu = sm.gmom[0]; rs = sm.gmom[1];
           } else {  // same doubles in the same member order as member_moments_w
@@ -521,17 +555,59 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
 #else
           const double2 acc = member_sums2(sm.gw, G, lane);
-          float mu, rs;
 #if TCN_FMOM
           gn_moments_f(acc.x, acc.y, a.inv_ch, 1e-8f, mu, rs);
 #else
           gn_moments(acc.x, acc.y, (double)CH * T, 1e-8f, mu, rs);
 #endif
 #endif
-          sc = rs * pm[PB_G1 + c];
-          sh = pm[PB_BE1 + c] - sc * mu;
         }
         if (TCN_SUB == 1) TPROBE(13);
+        float st[2] = {0.f, 0.f};
+        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
+#if TCN_DWP
+        // packed fp32: thread = input channels c2, c2+1 (hidden 2c2..2c2+3) x frames fr0..fr0+7
+        (void)c; (void)rh0;
+        const int c2 = 2 * (tid & (CH / 2 - 1)), fr0 = (tid >> 7) * (FR / 4);
+        const f32x2 sc2 = *reinterpret_cast<const f32x2*>(pm + PB_G1 + c2) * rs;
+        const f32x2 sh2 = *reinterpret_cast<const f32x2*>(pm + PB_BE1 + c2) - sc2 * mu;
+        f32x2 wv[2][3], bv[2];
+        dw_params2(pm, c2, wv, bv);
+        const float a2m1 = a2 - 1.f;
+        f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+        // rows fr0-D .. fr0+7+D of the pair once into registers (GN1 applied, zero outside [0, T)); H holds rows
+        // -4..35, so every load is in bounds and issued unconditionally
+        auto rows = [&](auto DC) {
+          constexpr int D = decltype(DC)::value;
+          const float* hb = lds_base(sm.H + (fr0 - D + 4) * CH + c2);
+          f32x2 hv[FR / 4 + 2 * D];
+#pragma unroll
+          for (int i = 0; i < FR / 4 + 2 * D; ++i) {
+            const int t = t0 + fr0 - D + i;
+            const float vm = (t >= 0 && t < T) ? 1.f : 0.f;  // mask multiply (a select sinks each load into a branch)
+            hv[i] = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(hb + i * CH), sc2, sh2) * vm;
+          }
+#pragma unroll
+          for (int i = 0; i < FR / 4; ++i) {
+            if (TCN_PFX && i < PD) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i);  // res_out ring entry i
+            const int tl = fr0 + i;
+            const float vo = t0 + tl < T ? 1.f : 0.f;
+            f32x2 y[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              f32x2 x = __builtin_elementwise_fma(wv[q][0], hv[i], bv[q]);
+              x = __builtin_elementwise_fma(wv[q][1], hv[i + D], x);
+              x = __builtin_elementwise_fma(wv[q][2], hv[i + 2 * D], x);
+              y[q] = prelu2(x, a2m1) * vo;
+              s0 += y[q];
+              s1 = __builtin_elementwise_fma(y[q], y[q], s1);
+            }
+            store_d4<PRE>(sm.Ahi + tl * LDD + 2 * c2, sm.Alo + tl * LDD + 2 * c2, y[0], y[1]);
+          }
+        };
+        static_assert(PD <= FR / 4, "one ring entry per frame of the packed depthwise conv");
+#else
+        const float sc = rs * pm[PB_G1 + c], sh = pm[PB_BE1 + c] - sc * mu;
         float wv[2][4];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -539,10 +615,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           wv[q][0] = pm[PB_WD + j * 3 + 0]; wv[q][1] = pm[PB_WD + j * 3 + 1]; wv[q][2] = pm[PB_WD + j * 3 + 2];
           wv[q][3] = pm[PB_BD + j];
         }
-        float st[2] = {0.f, 0.f};
         // rows rh0-D .. rh0+15+D of this channel once into registers (GN1 applied, zero outside [0, T));
         // H holds rows -4..35, so every load is in bounds and issued unconditionally
-        const __amdgpu_buffer_rsrc_t w2h = rsrc_of(wb + WL::W2H), w2l = rsrc_of(wb + WL::W2L);
         auto rows = [&](auto DC) {
           constexpr int D = decltype(DC)::value;
           float hv[FR / 2 + 2 * D];
@@ -575,12 +649,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             split_store2<PRE>(sm.Ahi, sm.Alo, tl * LDD + 2 * c, dv[0], dv[1]);
           }
         };
+#endif
         switch (dil) {
           case 1: rows(std::integral_constant<int, 1>{}); break;
           case 2: rows(std::integral_constant<int, 2>{}); break;
           case 3: rows(std::integral_constant<int, 3>{}); break;
           default: rows(std::integral_constant<int, 4>{}); break;
         }
+#if TCN_DWP
+        st[0] = s0.x + s0.y;
+        st[1] = s1.x + s1.y;
+#endif
         if (TCN_SUB == 1) TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
       TPROBE(4);
@@ -742,8 +821,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
         }
         const float afm = sm.af[m];
+#if TCN_PKE
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const f32x2 g2 = *reinterpret_cast<const f32x2*>(sm.at + trow(r)) * afm;  // frames trow(r), trow(r)+1
+          const f32x2 x = f32x2{rv[r], rv[r + 1]} * g2;
+          rv[r] = x.x; rv[r + 1] = x.y;
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) rv[r] = rv[r] * (afm * sm.at[trow(r)]);
+#endif
         if (bi == 0) {  // parity probe: TF_Attention output of block 0 (model/model.py:207)
           if (float* dp = DUMP ? kargs()->dump : nullptr) {
 #pragma unroll
@@ -759,6 +847,25 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #if TCN_MOM5
         {  // per-thread sums over its 16 rows first, then the channel weights once (same record, fewer VALU)
           float so = 0.f, soo = 0.f, su = 0.f, suu = 0.f, sou = 0.f;
+#if TCN_PKE
+          {
+            f32x2 so2 = {0.f, 0.f}, soo2 = so2, su2 = so2, suu2 = so2, sou2 = so2;
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const int tl = trow(r);
+              const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};  // masked, not branched
+              const f32x2 rp = vm * f32x2{rv[r], rv[r + 1]};
+              if constexpr (LM == LD_RECURSIVE) {
+                const f32x2 ov = vm * f32x2{o[r], o[r + 1]}, uv = ov + rp;
+                so2 += ov; soo2 = __builtin_elementwise_fma(ov, ov, soo2); su2 += uv;
+                suu2 = __builtin_elementwise_fma(uv, uv, suu2); sou2 = __builtin_elementwise_fma(ov, uv, sou2);
+              } else {
+                su2 += rp; suu2 = __builtin_elementwise_fma(rp, rp, suu2);
+              }
+            }
+            so = so2.x + so2.y; soo = soo2.x + soo2.y; su = su2.x + su2.y; suu = suu2.x + suu2.y; sou = sou2.x + sou2.y;
+          }
+#else
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int tl = trow(r);
@@ -771,6 +878,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               su += rp; suu = fmaf(rp, rp, suu);
             }
           }
+#endif
 #pragma unroll
           for (int j = 0; j < NMOM; ++j) mo[j] = 0.f;
           mo[2] = su; mo[3] = suu;
@@ -860,6 +968,18 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
+#if TCN_PKE
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          if (TCN_PFX) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
+          const int tl = trow(r);
+          const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r], rv[r + 1]}, kc);  // rv gated above
+          const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+          const f32x2 ov = x * vm;
+          o[r] = ov.x; o[r + 1] = ov.y;
+          split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn);
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
@@ -868,6 +988,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           o[r] = (t0 + tl < T) ? x : 0.f;
           split_store<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sxn);
         }
+#endif
       }
       __syncthreads();
       TPROBE(12);

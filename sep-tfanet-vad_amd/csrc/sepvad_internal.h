@@ -159,6 +159,7 @@ struct StftArgs {
   const float* gate_w;   // activity_input.weight [9], bias [9], prelu [10]
   float* S0;             // [B][Tp][CH] gated bins 1..256 (TCN input)
   double* gate_rec;      // [B][Tp/GATE_ROWS][2] TCN.LN partial statistics
+  int db_out;            // k_stft_gate: also store the dB spectrum (specdb) when the windows are equal (test entry)
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_stft_gate(const StftArgs& a, hipStream_t s);

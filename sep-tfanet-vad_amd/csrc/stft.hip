@@ -111,7 +111,7 @@ __global__ __launch_bounds__(SG_THREADS) void k_stft_gate(StftArgs a) {
         if (store_x && own) st_out(a.X + xrow * NBIN + k, Xk);
         if (store_db) {
           S[fi][k + 1] = live ? db : 0.f;
-          if (two && own) a.specdb[xrow * SPEC_LD + k] = db;
+          if ((two || a.db_out) && own) a.specdb[xrow * SPEC_LD + k] = db;
         }
       };
       const float2* rc = row + c;

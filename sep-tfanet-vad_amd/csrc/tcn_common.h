@@ -49,28 +49,45 @@ __device__ __forceinline__ void gputd(u64* p, unsigned tag, double v, bool l2) {
 __device__ __forceinline__ double dword2(unsigned lo, unsigned hi) {
   return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
 }
-// Poll the N words p[k] (nullptr = none) until every tag equals `tag`; values into v[k]. All loads of a
-// pass are in flight together. Bounded: gives up after a.spin_limit passes, or as soon as another
-// workgroup of this launch gave up (the device word then holds this launch's tag0), and records the give-up
-// in the device word and in its host-mapped copy; the launch then runs to completion with invalid outputs
-// instead of hanging, and the host reports it (sepvad_forward / sepvad_fused_status). Words of earlier
-// launches' give-ups hold other tags, so a give-up never leaks into a later launch.
+#ifndef TCN_POLL_SERIAL
+#define TCN_POLL_SERIAL 0
+#endif
+// A bounded hand-off wait gave up: record this launch's tag0 in the device word and its host-mapped copy.
 __device__ __forceinline__ void giveup(const TcnArgs& a) {
   __hip_atomic_store(a.err, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.herr != nullptr) __hip_atomic_store(a.herr, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Poll the N words p[k] (nullptr = none) until every tag equals tag[k]; values into v[k]. Every load of a pass is
+// unconditional (a null word reads a valid dummy word instead and is ignored), so all N are in flight together: a
+// load inside an exec-masked `if (p[k])` is waited for before the branch closes, which serialises the pass into N
+// round trips. Bounded: gives up after a.spin_limit passes, or as soon as another workgroup of this launch gave up
+// (the device word then holds this launch's tag0), and records the give-up in the device word and in its host-mapped
+// copy; the launch then runs to completion with invalid outputs instead of hanging, and the host reports it
+// (sepvad_forward / sepvad_fused_status; k_istft_pair writes NaN outputs). Words of earlier launches' give-ups hold
+// other tags, so a give-up never leaks into a later launch.
 template <int N>
-__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], const TcnArgs& a) {
+__device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned (&tag)[N], unsigned (&v)[N],
+                                       const TcnArgs& a) {
+  const u64* const dummy = a.gran;  // any readable 8-byte word
   unsigned spins = 0;
   for (;;) {
+    u64 x[N];
+#if TCN_POLL_SERIAL  // A/B switch: the round-2 form (each load inside its own `if (p[k])`: one round trip per word)
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      x[k] = 0;
+      if (p[k] != nullptr) x[k] = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    (void)dummy;
+#else
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = __hip_atomic_load(p[k] != nullptr ? p[k] : dummy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      if (p[k] != nullptr) {
-        const u64 x = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v[k] = (unsigned)x;
-        ok = ok && (unsigned)(x >> 32) == tag;
-      }
+      v[k] = (unsigned)x[k];
+      ok = ok && (p[k] == nullptr || (unsigned)(x[k] >> 32) == tag[k]);
     }
     if (ok) return;
     __builtin_amdgcn_s_sleep(1);
@@ -81,29 +98,12 @@ __device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, un
     }
   }
 }
-// gpoll with a tag per word (one round over words of different hand-offs)
 template <int N>
-__device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned (&tag)[N], unsigned (&v)[N],
-                                       const TcnArgs& a) {
-  unsigned spins = 0;
-  for (;;) {
-    bool ok = true;
+__device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, unsigned (&v)[N], const TcnArgs& a) {
+  unsigned tg[N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-      if (p[k] != nullptr) {
-        const u64 x = __hip_atomic_load(p[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v[k] = (unsigned)x;
-        ok = ok && (unsigned)(x >> 32) == tag[k];
-      }
-    }
-    if (ok) return;
-    __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 255u) == 0 &&
-        (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
-      giveup(a);
-      return;
-    }
-  }
+  for (int k = 0; k < N; ++k) tg[k] = tag;
+  gpollt<N>(p, tg, v, a);
 }
 
 // One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
@@ -134,6 +134,92 @@ __device__ __forceinline__ void split_store2(_Float16* hi, _Float16* lo, int idx
     *reinterpret_cast<f16x2*>(hi + idx) = f16x2{(_Float16)v0, (_Float16)v1};
   } else {
     *reinterpret_cast<bf16x2*>(hi + idx) = bf16x2{(__bf16)v0, (__bf16)v1};
+  }
+}
+
+// ---- packed fp32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two channels per instruction) ----
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) float lds_f32;
+// An LDS address the compiler must materialise in a VGPR: loads at constant distances from it then use the ds
+// instruction's 16-bit offset field (the H planes sit above 64 KB of LDS, so a folded constant base would not fit
+// and every load would get its own address add).
+__device__ __forceinline__ const float* lds_base(const float* p) {
+  unsigned a = (unsigned)(size_t)(const lds_f32*)p;
+  asm volatile("" : "+v"(a));
+  return (const float*)(const lds_f32*)(size_t)a;
+}
+// PReLU(x) = x > 0 ? x : a x, as x + (a - 1) min(x, 0) (a2m1 = a - 1): two v_min_f32 and one v_pk_fma_f32 per pair
+__device__ __forceinline__ f32x2 prelu2(f32x2 x, float a2m1) {
+  const f32x2 mn = {fminf(x.x, 0.f), fminf(x.y, 0.f)};
+  return __builtin_elementwise_fma(mn, f32x2{a2m1, a2m1}, x);
+}
+// Depthwise outputs of two adjacent input channels c, c+1 at one frame: y0 = (d[2c], d[2c+2]), y1 = (d[2c+1], d[2c+3])
+// (q = 0, 1 of each channel) -> hidden 2c..2c+3 as one 8-byte store per GEMM operand plane (PRE format as split_store)
+template <int PRE>
+__device__ __forceinline__ void store_d4(_Float16* hi, _Float16* lo, f32x2 y0, f32x2 y1) {
+  const f32x2 a = {y0.x, y1.x}, b = {y0.y, y1.y};  // hidden 2c, 2c+1 | 2c+2, 2c+3
+  if constexpr (PRE == PREC_F16X3) {
+    const f16x2v ha = __builtin_convertvector(a, f16x2v), hb = __builtin_convertvector(b, f16x2v);
+    const f16x2v la = __builtin_convertvector(a - __builtin_convertvector(ha, f32x2), f16x2v);
+    const f16x2v lb = __builtin_convertvector(b - __builtin_convertvector(hb, f32x2), f16x2v);
+    *reinterpret_cast<u32x2v*>(hi) = u32x2v{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+    *reinterpret_cast<u32x2v*>(lo) = u32x2v{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
+  } else if constexpr (PRE == PREC_F16) {
+    const f16x2v ha = __builtin_convertvector(a, f16x2v), hb = __builtin_convertvector(b, f16x2v);
+    *reinterpret_cast<u32x2v*>(hi) = u32x2v{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+  } else {
+    const bf16x2v ha = __builtin_convertvector(a, bf16x2v), hb = __builtin_convertvector(b, bf16x2v);
+    *reinterpret_cast<u32x2v*>(hi) = u32x2v{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+  }
+}
+// Two values of one channel at two frames (LDS rows idx and idx + ld) in the PRE format of split_store
+template <int PRE>
+__device__ __forceinline__ void split_store_rows(_Float16* hi, _Float16* lo, int idx, int ld, f32x2 v) {
+  if constexpr (PRE == PREC_F16X3) {
+    const f16x2v h = __builtin_convertvector(v, f16x2v);
+    const f16x2v l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2v);
+    hi[idx] = h.x; hi[idx + ld] = h.y;
+    lo[idx] = l.x; lo[idx + ld] = l.y;
+  } else if constexpr (PRE == PREC_F16) {
+    const f16x2v h = __builtin_convertvector(v, f16x2v);
+    hi[idx] = h.x; hi[idx + ld] = h.y;
+  } else {
+    const bf16x2v h = __builtin_convertvector(v, bf16x2v);
+    reinterpret_cast<__bf16*>(hi)[idx] = h.x; reinterpret_cast<__bf16*>(hi)[idx + ld] = h.y;
+  }
+}
+// resid_apply (device_common.h) on two frames of one channel: kc = {GN_a scale, shift, GN_b scale, shift}
+template <int MODE>
+__device__ __forceinline__ f32x2 resid_apply2(f32x2 o, f32x2 r, const float (&kc)[4]) {
+  const f32x2 k0 = {kc[0], kc[0]}, k1 = {kc[1], kc[1]};
+  if constexpr (MODE == LD_GN) {
+    return __builtin_elementwise_fma(o, k0, k1);
+  } else if constexpr (MODE == LD_RECURSIVE) {
+    const f32x2 v = o + __builtin_elementwise_fma(o + r, k0, k1);
+    return __builtin_elementwise_fma(v, f32x2{kc[2], kc[2]}, f32x2{kc[3], kc[3]});
+  } else if constexpr (MODE == LD_RESIDUAL) {
+    return o + __builtin_elementwise_fma(r, k0, k1);
+  } else if constexpr (MODE == LD_ADD) {
+    return o + r;
+  } else {
+    return o;
+  }
+}
+// Depthwise weights and bias of input channels c, c+1 (c even) from a parameter blob: wv[q][k] = (w[2c+q][k],
+// w[2c+2+q][k]), bv[q] = (b[2c+q], b[2c+2+q]). Scalar float reads (merged into wide LDS reads by the compiler):
+// pairs built from the elements of a u32x4 vector read miscompile on this toolchain (the packed FMA gets one element
+// broadcast through op_sel_hi).
+__device__ __forceinline__ void dw_params2(const float* pm, int c, f32x2 (&wv)[2][3], f32x2 (&bv)[2]) {
+  const float* wp = pm + PB_WD + 6 * c;
+  const float* bp = pm + PB_BD + 2 * c;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) wv[q][k] = f32x2{wp[3 * q + k], wp[6 + 3 * q + k]};
+    bv[q] = f32x2{bp[q], bp[2 + q]};
   }
 }
 

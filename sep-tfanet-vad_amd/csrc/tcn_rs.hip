@@ -33,6 +33,21 @@ constexpr int RS_LDX = CH + 8;     // x' row stride (halves): 132 dwords == 4 (m
 constexpr int RS_LDD = HID + 8;    // d row stride (halves): 260 dwords == 4 (mod 64)
 constexpr int RS_HS = CH + 2;      // H row stride (floats): rows 8 apart land 16 banks apart (depthwise reads)
 constexpr int RS_HROWS = FR + 8;   // H rows -4..35
+#ifndef RS_NOG2
+#define RS_NOG2 0                  // diagnostics: no res_out GEMM (wrong results; phase timing of the depthwise conv)
+#endif
+#ifndef RS_VPRIO
+#define RS_VPRIO 0                 // A/B: V waves at s_setprio 1
+#endif
+#ifndef RS_G2NOMFMA
+#define RS_G2NOMFMA 0              // diagnostics: res_out GEMM loads and waits without its MFMAs (wrong results)
+#endif
+#ifndef RS_G2NOLDS
+#define RS_G2NOLDS 0               // diagnostics: res_out GEMM without its A fragment reads (wrong results)
+#endif
+#ifndef RS_DW_SCALAR
+#define RS_DW_SCALAR 0             // A/B: the scalar depthwise conv
+#endif
 #ifndef RS_PD
 #define RS_PD 8                    // weight K steps in flight per M wave (two tiles, hi/lo: 16 KB per CU per step)
 #endif
@@ -138,9 +153,11 @@ __device__ __forceinline__ void mgemm(f32x16v& c0, f32x16v& c1, const _Float16* 
   for (int i = 0; i < NS; ++i) {
     const bool chunk_edge = G2 && (i + 1) % 8 == 0 && i + 1 < NS;
     f16x8 nh = ah, nl = al;
-    if (i + 1 < NS && !chunk_edge) afrag(i + 1, nh, nl);  // next step's A reads in flight during this step
+    if (!(G2 && RS_G2NOLDS) && i + 1 < NS && !chunk_edge) afrag(i + 1, nh, nl);  // next step's A reads in flight
     const int e = i % PD;
-    if constexpr (X3) {
+    if constexpr (G2 && RS_G2NOMFMA) {  // diagnostics: the res_out step without its MFMAs
+      asm volatile("" :: "v"(rh[e][0]), "v"(rh[e][1]), "v"(rl[e][0]), "v"(rl[e][1]), "v"(ah), "v"(al));
+    } else if constexpr (X3) {
       const f16x8 b0h = __builtin_bit_cast(f16x8, rh[e][0]), b1h = __builtin_bit_cast(f16x8, rh[e][1]);
       const f16x8 b0l = __builtin_bit_cast(f16x8, rl[e][0]), b1l = __builtin_bit_cast(f16x8, rl[e][1]);
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, b0h, c0, 0, 0, 0);
@@ -384,8 +401,20 @@ __device__ __forceinline__ void m_role(const TcnArgs& a, RsSmem& sm, const RsCtx
       for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
       {
         MLANE;
+#if RS_NOG2  // diagnostics only (wrong results): the M waves wait for the depthwise conv but run no res_out GEMM
+        {
+          const unsigned need = bc * NCH + NCH;
+          for (;;) {
+            const u32x4v f = *reinterpret_cast<const volatile u32x4v*>(sm.flag);
+            if (min(min(f[0], f[1]), min(f[2], f[3])) >= need) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          (void)ln;
+        }
+#else
         mgemm<NS2, RS_LDD, PRE, true>(acc0, acc1, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), VOFF2A,
                                       VOFF2A + NS2 * 1024, rh, rl, ln, sm.flag, bc * NCH, a);
+#endif
       }
       RPROBE(3);
       // raw sums of the res_out accumulator (the GN2 fold is applied after the exchange, by linearity): per channel
@@ -568,6 +597,58 @@ __device__ __forceinline__ void m_role(const TcnArgs& a, RsSmem& sm, const RsCtx
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// One depthwise chunk of one lane: d = PReLU(dconv(GN1(h))) (model/model.py:134-135) for input channels c, c+1 (hidden
+// 2c..2c+3) and frames 4f..4f+3, into the GEMM A planes; GN2 partial sums into s0/s1. MASK: zero padding of the
+// normalised input outside the utterance and zero output rows past its end (members at the utterance edges).
+template <int PRE, bool MASK>
+__device__ __forceinline__ void dw_chunk(RsSmem& sm, const float* pm, int c, int f, int dil, float mu1, float rs1,
+                                         float a2m1, int t0, int T, f32x2& s0, f32x2& s1) {
+  const f32x2 g1 = *reinterpret_cast<const f32x2*>(pm + PB_G1 + c), be1 = *reinterpret_cast<const f32x2*>(pm + PB_BE1 + c);
+  const f32x2 sc = g1 * rs1;
+  const f32x2 sh = be1 - sc * mu1;
+  f32x2 wv[2][3], bv[2];
+  dw_params2(pm, c, wv, bv);
+  const float* bl = lds_base(sm.H + (4 + 4 * f - dil) * RS_HS + c);
+  const float* bm = lds_base(sm.H + (4 + 4 * f) * RS_HS + c);
+  const float* br = lds_base(sm.H + (4 + 4 * f + dil) * RS_HS + c);
+  f32x2 xv[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xv[i][0] = *reinterpret_cast<const f32x2*>(bl + i * RS_HS);
+    xv[i][1] = *reinterpret_cast<const f32x2*>(bm + i * RS_HS);
+    xv[i][2] = *reinterpret_cast<const f32x2*>(br + i * RS_HS);
+  }
+  const int pr = prow(4 * f);  // rows 4f..4f+3 stay consecutive under prow
+  _Float16* const dh = sm.Ahi + pr * RS_LDD + 2 * c;
+  _Float16* const dl = sm.Alo + pr * RS_LDD + 2 * c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + 4 * f + i;
+    f32x2 h[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      h[k] = __builtin_elementwise_fma(xv[i][k], sc, sh);
+      if constexpr (MASK) {
+        const bool ok = (unsigned)(t + (k - 1) * dil) < (unsigned)T;
+        h[k] = ok ? h[k] : f32x2{0.f, 0.f};
+      }
+    }
+    f32x2 y[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f32x2 x = __builtin_elementwise_fma(wv[q][0], h[0], bv[q]);
+      x = __builtin_elementwise_fma(wv[q][1], h[1], x);
+      x = __builtin_elementwise_fma(wv[q][2], h[2], x);
+      f32x2 yy = prelu2(x, a2m1);
+      if constexpr (MASK) yy = (unsigned)t < (unsigned)T ? yy : f32x2{0.f, 0.f};
+      s0 += yy;
+      s1 = __builtin_elementwise_fma(yy, yy, s1);
+      y[q] = yy;
+    }
+    store_d4<PRE>(dh + i * RS_LDD, dl + i * RS_LDD, y[0], y[1]);
+  }
+}
+
 // V role (waves 4-7): next block parameters, every hand-off poll, the depthwise conv, the gates and moments.
 template <int LM, int PRE>
 __device__ __forceinline__ void v_role(const TcnArgs& a, RsSmem& sm, const RsCtx& x, int lane, int v, int wave_s) {
@@ -655,11 +736,10 @@ __device__ __forceinline__ void v_role(const TcnArgs& a, RsSmem& sm, const RsCtx
       RPROBE(10);
       // ---- d = PReLU(dconv(GN1(h))) (model/model.py:134-135), chunk by chunk into the A planes ----
       {
-        const float a2 = pm[PB_A2];
         const unsigned cid0 = bc * NCH;
         float st0 = 0.f, st1 = 0.f;
-        // runtime dilation: the three taps of a frame are read from H directly (one code path for every block,
-        // chunk loop not unrolled: the V role's code stays small next to the M role's in the instruction cache)
+#if RS_DW_SCALAR  // A/B: the first form (lane = channel x 8 frames, scalar VALU, the three taps read per frame)
+        const float a2 = pm[PB_A2];
         const int lo = -t0, span = T;  // frame tl is inside the utterance iff (unsigned)(tl - lo) < span
 #pragma unroll 1
         for (int j = 0; j < NCH; ++j) {
@@ -685,7 +765,6 @@ __device__ __forceinline__ void v_role(const TcnArgs& a, RsSmem& sm, const RsCtx
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int tl = 8 * fg + i;
-            // GN1 on load, zero padding outside the utterance
             const float h0 = (unsigned)(tl - dil - lo) < (unsigned)span ? fmaf(xv[i][0], sc, sh) : 0.f;
             const float h1 = (unsigned)(tl - lo) < (unsigned)span ? fmaf(xv[i][1], sc, sh) : 0.f;
             const float h2 = (unsigned)(tl + dil - lo) < (unsigned)span ? fmaf(xv[i][2], sc, sh) : 0.f;
@@ -709,6 +788,35 @@ __device__ __forceinline__ void v_role(const TcnArgs& a, RsSmem& sm, const RsCtx
           if (j == 1) RPROBE(14);
           if (j == 2) RPROBE(15);
         }
+#else
+        // lane (p = ln & 7, f = ln >> 3): input channels c, c+1 (c = 64v + 16j + 2p) x frames 4f..4f+3, packed fp32
+        // (v_pk_fma_f32 over the channel pair); members whose taps all lie inside the utterance skip the masks
+        f32x2 s0v = {0.f, 0.f}, s1v = {0.f, 0.f};
+        const float a2m1 = pm[PB_A2] - 1.f;
+        const bool inner = t0 - dil >= 0 && t0 + FR + dil <= T;
+        auto done = [&](int j) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this chunk's d in LDS before its flag
+          if (ln == 0) *reinterpret_cast<volatile unsigned*>(&sm.flag[v]) = cid0 + (unsigned)j + 1u;
+          if (j == 0) RPROBE(8);
+          if (j == 1) RPROBE(14);
+          if (j == 2) RPROBE(15);
+        };
+        if (inner) {
+#pragma unroll 1
+          for (int j = 0; j < NCH; ++j) {
+            dw_chunk<PRE, false>(sm, pm, 64 * v + 16 * j + 2 * (ln & 7), ln >> 3, dil, mu1, rs1, a2m1, t0, T, s0v, s1v);
+            done(j);
+          }
+        } else {
+#pragma unroll 1
+          for (int j = 0; j < NCH; ++j) {
+            dw_chunk<PRE, true>(sm, pm, 64 * v + 16 * j + 2 * (ln & 7), ln >> 3, dil, mu1, rs1, a2m1, t0, T, s0v, s1v);
+            done(j);
+          }
+        }
+        st0 = s0v.x + s0v.y;
+        st1 = s1v.x + s1v.y;
+#endif
         // GN2 partial sums: the last V wave publishes the member's (wave order, double) (P2)
         st0 = lane63_total(st0);
         st1 = lane63_total(st1);
@@ -886,6 +994,7 @@ __global__ __launch_bounds__(RS_NTHR) void k_tcn_rs(TcnArgs a) {
   // first block's parameter blob (later blocks: loaded one block ahead by the V waves)
   for (int k = tid; k < PB_SIZE / 4; k += RS_NTHR)
     reinterpret_cast<float4*>(sm.prm[0])[k] = reinterpret_cast<const float4*>(a.prm)[k];
+  if (RS_VPRIO && wave_s >= 4) __builtin_amdgcn_s_setprio(1);
   if (wave_s < 4) m_role<LM, PRE, DUMP>(a, sm, x, lane, wave_s, wave_s);
   else v_role<LM, PRE>(a, sm, x, lane, wave_s - 4, wave_s);
 }

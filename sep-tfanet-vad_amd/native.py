@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     "sepvad_forward_windows", "sepvad_pit_l1_sums", "sepvad_pit_l1_choose",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
     "sepvad_last_forward", "sepvad_side_outputs_of", "sepvad_release_stream",
+    "sepvad_stft_gate_test", "sepvad_istft_pair_test",
     "sepvad_stft", "sepvad_istft",
     "sepvad_pit_l1", "sepvad_stream_append",
     "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_vad_accuracy",
@@ -104,6 +105,10 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_side_outputs_of.argtypes = [P, ctypes.POINTER(SepVadOutputs), P, ctypes.c_int64, i32, i32]
     lib.sepvad_release_stream.restype = i32
     lib.sepvad_release_stream.argtypes = [P, P]
+    lib.sepvad_stft_gate_test.restype = i32
+    lib.sepvad_stft_gate_test.argtypes = [P, P, i32, i32, P, P, P]
+    lib.sepvad_istft_pair_test.restype = i32
+    lib.sepvad_istft_pair_test.argtypes = [P, P, P, i32, i32, P, P, P]
     lib.sepvad_stft.restype = i32
     lib.sepvad_stft.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft.restype = i32
@@ -385,6 +390,35 @@ class Handle:
         spec = torch.empty(B, 257, T, device=self.device, dtype=torch.float32)
         _check(self._lib.sepvad_stft(self._h, _ptr(x), B, N, _ptr(X), _ptr(spec), self._stream()), "sepvad_stft")
         return X, spec
+
+    def stft_fused(self, x: torch.Tensor):
+        """The forward's own front end (k_stft_gate, sepvad_stft_gate_test): (X [B, 257, T] complex64 with DC
+        zeroed, its dB spectrum [B, 257, T]) from the frame-major workspace layout."""
+        x = x.to(self.device, torch.float32).contiguous()
+        B, N = x.shape
+        T = 1 + N // 256
+        Tp = (T + 63) // 64 * 64
+        X = torch.zeros(B, Tp, 257, device=self.device, dtype=torch.complex64)
+        db = torch.zeros(B, Tp, 260, device=self.device, dtype=torch.float32)
+        _check(self._lib.sepvad_stft_gate_test(self._h, _ptr(x), B, N, _ptr(X), _ptr(db), self._stream()),
+               "sepvad_stft_gate_test")
+        return X[:, :T].transpose(1, 2), db[:, :T, :257].transpose(1, 2)
+
+    def istft_pair(self, X: torch.Tensor, masks: torch.Tensor, N: int):
+        """The forward's own back end (k_istft_pair, sepvad_istft_pair_test): for X [B, 257, T] complex and
+        pre-sigmoid masks [B, 2, 257, T], est = X sigmoid(masks) [B, 2, 257, T] and y = istft(est, length=N)
+        [B, 2, N]."""
+        B, F, T = X.shape
+        Tp = (T + 63) // 64 * 64
+        Xf = torch.zeros(B, Tp, 257, device=self.device, dtype=torch.complex64)
+        Xf[:, :T] = X.to(self.device, torch.complex64).transpose(1, 2)
+        mf = torch.zeros(B, Tp, 576, device=self.device, dtype=torch.float32)
+        mf[:, :T, :514] = masks.to(self.device, torch.float32).reshape(B, 514, T).transpose(1, 2)
+        y = torch.empty(B, 2, N, device=self.device, dtype=torch.float32)
+        est = torch.empty(B, 2, 257, T, device=self.device, dtype=torch.complex64)
+        _check(self._lib.sepvad_istft_pair_test(self._h, _ptr(Xf), _ptr(mf), B, N, _ptr(y), _ptr(est), self._stream()),
+               "sepvad_istft_pair_test")
+        return y, est
 
     def istft(self, est: torch.Tensor, N: int):
         """torch.istft(center=True, length=N) of est [BS, 257, T] complex64 (kernel-level test entry)."""
