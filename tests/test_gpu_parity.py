@@ -102,6 +102,181 @@ def test_forward_matches_reference(cname, case, models):
     assert not fails, "; ".join(fails)
 
 
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_inference_kw_smoothed_vad(cname, models):
+    g = load_golden(cname, "small")
+    ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+               threshold_activated_vad=0.5, return_smoothed_vad=True)
+    with torch.no_grad():
+        sep, vad, _ = models[cname](torch.from_numpy(g["x"]).to(DEV), ikw)
+    assert tuple(vad.shape) == g["ikw_vad"].shape  # [B, 2, 1, T]
+    assert np.array_equal(vad.cpu().numpy(), g["ikw_vad"])
+    assert np.abs(sep.cpu().numpy() - g["ikw_sep"]).max() <= SEP_TOL
+
+
+def test_inference_kw_variants_vs_oracle(models, state_dicts):
+    """unsmoothed-filter flag, threshold, length_smoothing_filter=5 (no effect) vs the oracle."""
+    from oracle.torch_ref import OracleModel
+    g = load_golden("with_vad", "small")
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"])
+    x = torch.from_numpy(g["x"])
+    for ikw in (dict(filter_signals_by_smo_vad=False, filter_signals_by_unsmo_vad=True, length_smoothing_filter=5,
+                     threshold_activated_vad=0.4, return_smoothed_vad=False),
+                dict(filter_signals_by_smo_vad=False, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
+                     threshold_activated_vad=0.6, return_smoothed_vad=True)):
+        s_ref, v_ref, _ = om(x, ikw)
+        with torch.no_grad():
+            s, v, _ = models["with_vad"](x.to(DEV), ikw)
+        assert tuple(v.shape) == tuple(v_ref.shape)
+        assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+        if ikw["return_smoothed_vad"]:
+            assert np.array_equal(v.cpu().numpy(), v_ref.numpy())
+
+
+def test_stft_kernel_vs_torch(models):
+    """STFT kernel vs torch.stft (fp32, on the GPU) — the op torchaudio.Spectrogram runs."""
+    h = models["with_vad"].native_handle(DEV)
+    for N in (8000, 12345, 32000, 257):
+        x = torch.rand(3, N, device=DEV) * 1.8 - 0.9
+        X, spec = h.stft(x)
+        win = torch.hann_window(512, device=DEV)
+        Xr = torch.stft(x, 512, 256, 512, win, center=True, pad_mode="reflect", normalized=False, onesided=True,
+                        return_complex=True)
+        Xr[:, 0, :] = 0
+        assert X.shape == Xr.shape
+        assert (X - Xr).abs().max().item() <= 2e-5 * Xr.abs().max().item() + 1e-5
+        sr = 10 * torch.log10(torch.clamp(Xr.abs() ** 2, min=1e-10))
+        ok = Xr.abs() > 1e-2  # dB of tiny bins amplifies fp32 rounding (d dB = 8.7 |dX|/|X|)
+        assert (spec - sr)[ok].abs().max().item() <= 2e-3
+
+
+def test_istft_kernel_vs_torch(models):
+    h = models["with_vad"].native_handle(DEV)
+    for N in (8000, 12345, 32000):
+        T = 1 + N // 256
+        est = torch.randn(4, 257, T, device=DEV, dtype=torch.complex64)
+        y = h.istft(est, N)
+        win = torch.hann_window(512, device=DEV)
+        yr = torch.istft(est, 512, 256, 512, win, center=True, normalized=False, onesided=True, length=N)
+        assert (y - yr).abs().max().item() <= 1e-5 * max(1.0, yr.abs().max().item())
+
+
+def test_stft_istft_round_trip(models):
+    h = models["with_vad"].native_handle(DEV)
+    x = torch.rand(2, 32000, device=DEV) * 1.8 - 0.9
+    X, _ = h.stft(x)
+    # DC was removed: the round trip reproduces x minus its per-frame DC contribution; compare with torch
+    win = torch.hann_window(512, device=DEV)
+    yr = torch.istft(X, 512, 256, 512, win, center=True, length=32000)
+    y = h.istft(X, 32000)
+    assert (y - yr).abs().max().item() <= 1e-5
+
+
+PROD_N = (257, 8000, 12345, 32000, 261888)
+
+
+@pytest.mark.parametrize("N", PROD_N)
+def test_stft_gate_kernel_vs_torch(models, N):
+    """The forward's own front end, k_stft_gate (sepvad_stft_gate_test), vs torch.stft + AmplitudeToDB
+    (model/model.py:16-25,408-412): X within 2e-5 of its range, dB within 2e-3 on bins |X| > 1e-2 (d dB =
+    8.7 |dX| / |X|), T = 2 .. 1024 frames."""
+    h = models["with_vad"].native_handle(DEV)
+    B = 3 if N <= 32000 else 1
+    g = torch.Generator(device="cpu").manual_seed(N)
+    x = (torch.rand(B, N, generator=g) * 1.8 - 0.9).to(DEV)
+    X, db = h.stft_fused(x)
+    win = torch.hann_window(512, device=DEV)
+    Xr = torch.stft(x, 512, 256, 512, win, center=True, pad_mode="reflect", normalized=False, onesided=True,
+                    return_complex=True)
+    Xr[:, 0, :] = 0
+    assert X.shape == Xr.shape and db.shape == Xr.shape
+    assert (X - Xr).abs().max().item() <= 2e-5 * Xr.abs().max().item() + 1e-5
+    sr = 10 * torch.log10(torch.clamp(Xr.abs() ** 2, min=1e-10))
+    ok = Xr.abs() > 1e-2
+    ok[:, 0, :] = True  # DC: -100 dB in both
+    assert (db - sr)[ok].abs().max().item() <= 2e-3
+
+
+@pytest.mark.parametrize("N", PROD_N)
+def test_istft_pair_kernel_vs_torch(models, N):
+    """The forward's own back end, k_istft_pair (sepvad_istft_pair_test): est = X sigmoid(m) per speaker within
+    1e-6 of its range and y = torch.istft(est, length=N) within 1e-5 (model/model.py:429-460), X the DC-zeroed
+    STFT of a real signal (as in the forward), pre-sigmoid masks in [-6, 6]."""
+    h = models["with_vad"].native_handle(DEV)
+    B = 2 if N <= 32000 else 1
+    g = torch.Generator(device="cpu").manual_seed(7 + N)
+    x = (torch.rand(B, N, generator=g) * 1.8 - 0.9).to(DEV)
+    win = torch.hann_window(512, device=DEV)
+    X = torch.stft(x, 512, 256, 512, win, center=True, pad_mode="reflect", return_complex=True)
+    X[:, 0, :] = 0
+    T = X.shape[-1]
+    m = (torch.rand(B, 2, 257, T, generator=g) * 12 - 6).to(DEV)
+    y, est = h.istft_pair(X, m, N)
+    er = X[:, None] * torch.sigmoid(m)
+    assert (est - er).abs().max().item() <= 1e-6 * er.abs().max().item()
+    yr = torch.istft(er.reshape(B * 2, 257, T), 512, 256, 512, win, center=True, length=N).reshape(B, 2, N)
+    assert (y - yr).abs().max().item() <= 1e-5 * max(1.0, yr.abs().max().item())
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_full_batch_properties(cname, models, state_dicts):
+    """BASELINE cfg shape B=64, N=32000: a sample of utterances vs the oracle, batch invariance
+    (bitwise), determinism, and SI-SDR within 0.01 dB of the oracle against the clean sources."""
+    from oracle.torch_ref import OracleModel, si_sdr
+    from sep_tfanet_vad_amd import synth
+    B, N = 64, 32000
+    x, srcs = synth.make_batch(B, N, 5000)
+    xd = torch.from_numpy(x).to(DEV)
+    net = models[cname]
+    with torch.no_grad():
+        sep, vad, est = net(xd)
+        sep2, vad2, _ = net(xd)
+        sub = [0, 17, 63]
+        sep_sub, vad_sub, _ = net(xd[sub])
+    torch.cuda.synchronize()
+    assert torch.equal(sep, sep2) and torch.equal(vad, vad2)           # deterministic
+    assert torch.equal(sep[sub], sep_sub) and torch.equal(vad[sub], vad_sub)  # batch invariant
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    s_ref, v_ref, _ = om(torch.from_numpy(x[sub]))
+    assert np.abs(sep_sub.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((vad_sub.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    # SI-SDR (reference model/combined_loss.py:16-56) of each output vs the matching source
+    tgt = torch.from_numpy(srcs[sub])
+    d = (si_sdr(sep_sub.cpu(), tgt) - si_sdr(s_ref, tgt)).abs().max().item()
+    assert d <= 0.01, f"SI-SDR differs by {d} dB"
+
+
+def test_streams_and_devices_do_not_leak_state(models):
+    """Two handles / back-to-back shapes: results depend only on the inputs."""
+    g = load_golden("with_vad", "ragged")
+    net = models["with_vad"]
+    with torch.no_grad():
+        a, _, _ = net(torch.from_numpy(g["x"]).to(DEV))
+        net(torch.rand(5, 48000, device=DEV))  # grow the workspace
+        b, _, _ = net(torch.from_numpy(g["x"]).to(DEV))
+    assert torch.equal(a, b)
+
+
+def test_batch_split_is_bitwise_identical(models):
+    """sepvad_set_split: utterance chunks on concurrent internal streams give the same bits."""
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(13, 20000, 900)[0]).to(DEV)
+    net = models["with_vad"]
+    h = net.native_handle(DEV)
+    outs = []
+    for n in (1, 2, 3, 4):
+        h.set_split(n)
+        with torch.no_grad():
+            sep, vad, est = net(x)
+        outs.append((sep.clone(), vad.clone(), est.clone(), net.masks_b.clone(), net.spectrum.clone()))
+    h.set_split(1)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 def test_strided_windows_match_contiguous(models):
     """forward on strided row views (streaming windows) == forward on their contiguous copies."""
     from sep_tfanet_vad_amd import synth
