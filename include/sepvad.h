@@ -153,6 +153,12 @@ int32_t sepvad_last_forward(sepvad_handle h, void* stream, int64_t* seq, int32_t
 int32_t sepvad_side_outputs_of(sepvad_handle h, const SepVadOutputs* out, void* stream, int64_t seq, int32_t B,
                                int32_t N);
 
+/* Diagnostics: with SEPVAD_TCN_CLOCK=1 in the environment every k_tcn launch records {~(min start), max end (100 MHz
+ * wall clock over all workgroups), workgroup 0: start / end wall clock, start / end shader clock (s_memtime), 0, 0}.
+ * Synchronises the device and copies the last min(max_records, recorded) records, oldest first, as 8 uint64 each;
+ * *n = records available (at most 4096). */
+int32_t sepvad_tcn_clock(sepvad_handle h, uint64_t* out, int32_t max_records, int32_t* n);
+
 /* Synchronises `stream` and frees the per-stream context (workspace, hand-off words, pinned give-up word) the handle
  * holds for it. Contexts are otherwise kept (at most SEPVAD_MAX_STREAM_CTX = 32 per handle by default, the least
  * recently used evicted after a sync of its stream). */

@@ -96,6 +96,7 @@ Workspace ws_view(const Workspace& w, int b0, int Tp) {
 }
 
 constexpr int MAX_SPLIT = 4;
+constexpr int TCLK_RECS = 4096;  // SEPVAD_TCN_CLOCK records kept (ring)
 
 // Per caller-stream state (include/sepvad.h: concurrent forwards on different streams of one handle are
 // allowed): the workspace, the fused TCN's hand-off words, launch salt and give-up words. Weights are
@@ -162,6 +163,8 @@ struct sepvad_model {
   int res_B = 0, res_N = 0;     // sepvad_reserve hint: every context's workspace is sized at least this
   unsigned long long* kprobe = nullptr;  // SEPVAD_TAIL_PROBE diagnostics: [workgroups][8]
   unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
+  unsigned long long* tclk = nullptr;    // SEPVAD_TCN_CLOCK diagnostics: [TCLK_RECS][8] per-launch clock records
+  long long tclk_n = 0;                  // k_tcn launches recorded so far
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;
@@ -412,7 +415,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
   for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
     // co-resident workgroups of the persistent TCN kernel that will run (both use one 512-thread workgroup per CU)
-    h->tcn_cap_p[p] = ncu * std::min(tcn_blocks_per_cu(ln, p), tcn_rs_blocks_per_cu(ln, p));
+    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
   }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
@@ -979,9 +982,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
-    // SEPVAD_TCN_IMPL: 0 (default) = k_tcn (fused.hip), 1 = k_tcn_rs (role-specialised waves, tcn_rs.hip)
-    const bool rs_impl = env_int("SEPVAD_TCN_IMPL", 0) != 0;
-    auto launch_t = [&](const TcnArgs& t, int grid) { return rs_impl ? launch_tcn_rs(t, grid, s) : launch_tcn(t, grid, s); };
+    auto launch_t = [&](const TcnArgs& t, int grid) { return launch_tcn(t, grid, s); };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     int ngroups = std::min(B, h->tcn_cap_p[h->prec] / G);
@@ -1028,6 +1029,15 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
           ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
           ++gsalt_n;
         }
+      }
+      ta.clk = nullptr;
+      if (env_int("SEPVAD_TCN_CLOCK", 0)) {  // diagnostics: per-launch span and shader clock (sepvad_tcn_clock)
+        if (!h->tclk) {
+          HIPCHK(hipMalloc(&h->tclk, (size_t)TCLK_RECS * 8 * sizeof(unsigned long long)));
+          HIPCHK(hipMemset(h->tclk, 0, (size_t)TCLK_RECS * 8 * sizeof(unsigned long long)));
+        }
+        ta.clk = h->tclk + (size_t)(h->tclk_n++ % TCLK_RECS) * 8;
+        HIPCHK(hipMemsetAsync(ta.clk, 0, 8 * sizeof(unsigned long long), s));
       }
       if (ev()) return SEPVAD_E_HIP;
       HIPCHK(launch_t(ta, ngl * G));
@@ -1374,6 +1384,25 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
   return rc;
 }
 
+int32_t sepvad_tcn_clock(sepvad_handle h, uint64_t* out, int32_t max_records, int32_t* n) {
+  if (!h || !n || (max_records > 0 && !out)) return fail(SEPVAD_E_ARG, "sepvad_tcn_clock: null argument");
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIPCHK(hipDeviceSynchronize());
+  const long long have = std::min<long long>(h->tclk_n, TCLK_RECS);
+  const int k = (int)std::min<long long>(have, std::max(0, max_records));
+  *n = (int)have;
+  if (k > 0) {  // the last k records, oldest first
+    std::vector<unsigned long long> all((size_t)TCLK_RECS * 8);
+    HIPCHK(hipMemcpy(all.data(), h->tclk, all.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int i = 0; i < k; ++i) {
+      const long long r = (h->tclk_n - k + i) % TCLK_RECS;
+      for (int j = 0; j < 8; ++j) out[(size_t)i * 8 + j] = all[(size_t)r * 8 + j];
+    }
+  }
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_last_forward(sepvad_handle h, void* stream, int64_t* seq, int32_t* B, int32_t* N) {
   if (!h || !seq || !B || !N) return fail(SEPVAD_E_ARG, "sepvad_last_forward: null argument");
   std::lock_guard<std::mutex> lk(h->mu);
@@ -1637,6 +1666,7 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
+  if (h->tclk) (void)hipFree(h->tclk);
   if (h->kprobe) (void)hipFree(h->kprobe);
   if (h->dparams) (void)hipFree(h->dparams);
   if (h->dhalf) (void)hipFree(h->dhalf);

@@ -65,10 +65,16 @@ namespace sepvad {
 #define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)
 #endif
 #ifndef TCN_DWP
-#define TCN_DWP 0    // depthwise conv in packed fp32 over channel pairs (1) or one channel per thread, scalar (0)
+#define TCN_DWP 1    // depthwise conv in packed fp32 over channel pairs (1) or one channel per thread, scalar (0)
 #endif
 #ifndef TCN_PKE
-#define TCN_PKE 0    // elementwise phases (epilogue, gates, moments, x' update) in packed fp32 over row pairs (1)
+#define TCN_PKE 1    // elementwise phases (epilogue, gates, moments, x' update) in packed fp32 over row pairs (1)
+#endif
+#ifndef TCN_M23
+#define TCN_M23 1    // GN2 statistics (P2) and TF-attention sums (P3) in one hand-off round, sums on the raw accumulator
+#endif
+#if TCN_M23 && !TCN_GNW
+#error "TCN_M23 finishes the GN2 moments in the polling wave (TCN_GNW)"
 #endif
 #ifndef TCN_EPI
 #define TCN_EPI 1    // conv1d epilogue parameters from global into registers: no barrier before the epilogue
@@ -300,6 +306,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (a.nblk > 5) a.probe[((size_t)blockIdx.x * a.nblk + 3) * 16 + 15] = __builtin_amdgcn_s_memtime();
   }
   if (a.force_err && blockIdx.x == 0 && threadIdx.x == 0) giveup(a);  // diagnostics: report path only
+  if (a.clk != nullptr && threadIdx.x == 0) {  // diagnostics (SEPVAD_TCN_CLOCK): launch span and shader clock
+    const unsigned long long rt = wall_clock64();
+    __hip_atomic_fetch_max(a.clk, ~rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) { a.clk[2] = rt; a.clk[4] = __builtin_amdgcn_s_memtime(); }
+  }
   if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact
     if (tid < CH) sm.af[tid] = 1.f;
     if (tid < FR) sm.at[tid] = 1.f;
@@ -674,6 +685,128 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
       TPROBE(5);
       }
+#if TCN_M23
+      f32x16v& rv = acc;  // r = res_out output, in place
+      const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
+      // GN2 {mean, rstd} of the group from the polled P2 words (a wave's lanes base.. or the words in LDS)
+      auto gn2_moments = [&](float& fmu, float& frs) {
+        if (G <= FG_WAVE) {
+          fmu = sm.gmom[2]; frs = sm.gmom[3];
+        } else {
+          const double2 sums = member_sums2(sm.gw, G, lane);
+          gn_moments_f(sums.x, sums.y, a.inv_hid, pm[PB_EPS2], fmu, frs);  // eps rescaled with d
+        }
+      };
+      if (!tf) {  // no TF-attention sums to exchange: the P2 round alone
+        const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
+        unsigned v[1];
+        gpoll<1>(p, tag2, v, a);
+        if (G <= FG_WAVE) {
+          if (wave_s == 0) {
+            float mu, rs;
+            member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
+            if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
+          }
+        } else if (tid < 4 * G) {
+          sm.gw[tid] = v[0];
+        }
+        __syncthreads();
+      TPROBE(6);
+        float fmu, frs;
+        gn2_moments(fmu, frs);
+        const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
+      }
+      // ---- TF_Attention (model/model.py:182-208) ----
+      if (tf) {
+        // P2 + P3 in ONE hand-off round: the row / column sums are taken on the raw res_out accumulator and the
+        // GN2 fold (affine per channel) is applied to the exchanged sums, so they need not wait for the GN2 words
+        {
+          const float ws = pm[PB_WS2 + m];
+          float rsum = 0.f, csr[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            rsum += t0 + trow(r) < T ? acc[r] : 0.f;
+            csr[r] = half_total(ws * acc[r]);  // ws-weighted sum over the wave's 32 channels (lanes 31 / 63)
+          }
+          if ((lane & 31) == 31) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm.cs[trow(r)][wave] = csr[r];
+          }
+          rsum += __shfl_xor(rsum, 32);
+          if (hl == 0) gputf(slot(g, e3) + GW_ROW + m, tag3, rsum, l2);
+        }
+        __syncthreads();  // cs complete; also: every wave is done reading d from LDS
+      TPROBE(6);
+        if (tid < FR) {  // P3 words: per-frame raw channel sums (a_t)
+          float s = 0.f;
+#pragma unroll
+          for (int sl = 0; sl < 8; ++sl) s += sm.cs[tid][sl];
+          sm.csum[tid] = s;
+          gputf(slot(g, e3) + GW_COL + tid, tag3, s, l2);
+        }
+      TPROBE(7);
+        {
+          const u64* pp[FG_CHUNK];
+          unsigned v[FG_CHUNK], tg[FG_CHUNK];
+          int mi = -1;  // a_t input index (frame t0 - 4 + mi) served by this thread
+          const u64* pat = nullptr;
+          if (tid >= CH && tid < CH + 8) {
+            const int k = tid - CH;
+            mi = k < 4 ? k : FR + k;             // 0..3 and 36..39
+            const int tl = mi - 4, t = t0 + tl;
+            if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
+          }
+          const int kq = tid - (NTHR - 128);  // threads 384..: GN2 word kq of the 4G (wave 6 holds all of them for G <= 16)
+          const u64* pq = (kq >= 0 && kq < 4 * G) ? slot(kq >> 2, e2) + GW_STAT + (kq & 3) : nullptr;
+          float s = 0.f, vat = 0.f;
+          unsigned vq = 0u;
+          for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
+#pragma unroll
+            for (int mm = 0; mm < FG_CHUNK; ++mm) {
+              pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
+              tg[mm] = tag3;
+            }
+            if (c0 == 0 && mi >= 0) pp[0] = pat;
+            if (c0 == 0 && kq >= 0) { pp[0] = pq; tg[0] = tag2; }
+            gpollt<FG_CHUNK>(pp, tg, v, a);
+            if (tid < CH) {
+#pragma unroll
+              for (int mm = 0; mm < FG_CHUNK; ++mm)
+                if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
+            }
+            if (c0 == 0) { vat = __builtin_bit_cast(float, v[0]); vq = v[0]; }
+          }
+          if (G <= FG_WAVE) {
+            if (wave_s == 6) {
+              float mu, rs;
+              member_moments_w(vq, 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
+              if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
+            }
+          } else if (kq >= 0 && kq < 4 * G) {
+            sm.gw[kq] = vq;
+          }
+          __syncthreads();  // csum, the GN2 moments / words complete
+          float fmu, frs;
+          gn2_moments(fmu, frs);
+          const float Tf = (float)T, sfc = pm[PB_SFC2], sb = pm[PB_SB2];
+          if (tid < CH) {  // a_f input: channel means of r over the utterance (GN2 fold applied to the sums)
+            sm.vec[tid + 4] = (frs * (pm[PB_WS2 + tid] * s - Tf * fmu * pm[PB_FC2 + tid]) + Tf * pm[PB_B2 + tid]) / Tf;
+            if (tid < 4) { sm.vec[tid] = 0.f; sm.vec[CH + 4 + tid] = 0.f; sm.yf[tid] = 0.f; sm.yf[CH + 4 + tid] = 0.f; }
+          } else if (mi >= 0) {
+            sm.mC[mi] = pat != nullptr ? (frs * (vat - fmu * sfc) + sb) / (float)CH : 0.f;
+          } else if (tid >= CH + 8 && tid < CH + 8 + FR) {
+            const int tl = tid - CH - 8;
+            sm.mC[tl + 4] = (t0 + tl < T) ? (frs * (sm.csum[tl] - fmu * sfc) + sb) / (float)CH : 0.f;
+          }
+          const float ws = pm[PB_WS2 + m], bias = pm[PB_B2 + m], fcm = fmu * pm[PB_FC2 + m];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rv[r] = fmaf(frs, fmaf(rv[r], ws, -fcm), bias);
+        }
+        __syncthreads();
+      TPROBE(8);
+#else
       {
         const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
         unsigned v[1];
@@ -788,6 +921,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
         __syncthreads();
       TPROBE(8);
+#endif
         const float* p = pm + PB_ATT;
         // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the channel axis);
         // a_t: mean over channels -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (over the frame axis)
@@ -1012,6 +1146,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       block_sums<2>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
       __syncthreads();
     }
+  }
+  if (a.clk != nullptr && threadIdx.x == 0) {
+    const unsigned long long rt = wall_clock64();
+    if (blockIdx.x == 0) { a.clk[3] = rt; a.clk[5] = __builtin_amdgcn_s_memtime(); }
+    __hip_atomic_fetch_max(a.clk + 1, rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -279,7 +279,7 @@ constexpr int FR = 32;          // frames per workgroup
 constexpr int FG_MAX = 32;      // workgroups per utterance (T <= 1024: 16.4 s at 16 kHz in one fused forward)
 constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
 constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
-constexpr int NGR = 2368;       // 8-byte {tag, value} hand-off words per slot (k_tcn: >= 4 + 8 * 256; k_tcn_rs: 2367)
+constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
 constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
 constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine
@@ -316,14 +316,12 @@ struct TcnArgs {
   int xmode;             // hand-off protocol: 0 = L2-resident when a group shares one XCD, else write-through;
                          // 1 = always write-through (tests)
   unsigned long long* probe;  // diagnostics: [grid][nblk][16] phase timestamps (nullable)
+  unsigned long long* clk;    // diagnostics (SEPVAD_TCN_CLOCK), nullable: this launch's record {~min start, max end
+                              // (100 MHz wall clock), workgroup 0: start, end wall clock, start, end shader clock}
   float* dump;           // parity probe (sepvad_set_tcn_dump), nullable: [3][B][Tp][CH] = TCN.LN output x'_0,
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
-// The same TCN as ONE persistent launch with role-specialised waves (tcn_rs.hip: matrix waves run the GEMMs,
-// vector waves the depthwise conv, polls and gates); same arguments, outputs and hand-off buffer.
-hipError_t launch_tcn_rs(const TcnArgs& a, int grid, hipStream_t s);
-int tcn_rs_blocks_per_cu(int ln_mode, int prec);
 // Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
 // for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
 struct HeadArgs {

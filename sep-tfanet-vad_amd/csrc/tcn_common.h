@@ -1,4 +1,4 @@
-// Device helpers shared by the two persistent TCN kernels (fused.hip k_tcn, tcn_rs.hip k_tcn_rs):
+// Device helpers of the persistent TCN kernel (fused.hip k_tcn):
 // MFMA operand types, wave-uniform buffer descriptors, the tagged 8-byte hand-off words ("data is its own
 // flag", cdna_hip_programming.md Guideline 16 R2) with bounded polls, DPP lane reductions and the fp16 hi/lo
 // operand split.

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
     "sepvad_forward_windows", "sepvad_pit_l1_sums", "sepvad_pit_l1_choose",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
-    "sepvad_last_forward", "sepvad_side_outputs_of", "sepvad_release_stream",
+    "sepvad_last_forward", "sepvad_side_outputs_of", "sepvad_release_stream", "sepvad_tcn_clock",
     "sepvad_stft_gate_test", "sepvad_istft_pair_test",
     "sepvad_stft", "sepvad_istft",
     "sepvad_pit_l1", "sepvad_stream_append",
@@ -105,6 +105,8 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_side_outputs_of.argtypes = [P, ctypes.POINTER(SepVadOutputs), P, ctypes.c_int64, i32, i32]
     lib.sepvad_release_stream.restype = i32
     lib.sepvad_release_stream.argtypes = [P, P]
+    lib.sepvad_tcn_clock.restype = i32
+    lib.sepvad_tcn_clock.argtypes = [P, P, i32, ctypes.POINTER(i32)]
     lib.sepvad_stft_gate_test.restype = i32
     lib.sepvad_stft_gate_test.argtypes = [P, P, i32, i32, P, P, P]
     lib.sepvad_istft_pair_test.restype = i32
@@ -363,6 +365,21 @@ class Handle:
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         _check(self._lib.sepvad_release_stream(self._h, ctypes.c_void_p(stream)), "sepvad_release_stream")
+
+    def tcn_clock(self, max_records: int = 4096):
+        """Per-launch k_tcn clock records (diagnostics; needs SEPVAD_TCN_CLOCK=1 when the forwards ran):
+        numpy [n, 3] of (launch span us, workgroup 0 span us, workgroup 0 shader clock MHz), oldest first."""
+        import numpy as np
+        buf = (ctypes.c_uint64 * (8 * max_records))()
+        n = ctypes.c_int32(0)
+        _check(self._lib.sepvad_tcn_clock(self._h, buf, max_records, ctypes.byref(n)), "sepvad_tcn_clock")
+        k = min(n.value, max_records)
+        u = np.frombuffer(buf, dtype=np.uint64, count=8 * k).reshape(k, 8)
+        span = (u[:, 1] - ~u[:, 0]).astype(np.float64) / 100.0  # the min start is stored as a max of complements
+        r = u.astype(np.float64)
+        w0 = (r[:, 3] - r[:, 2]) / 100.0
+        mhz = (r[:, 5] - r[:, 4]) / np.maximum(w0, 1e-9)
+        return np.stack([span, w0, mhz], axis=1)
 
     def tcn_dump(self, x: torch.Tensor):
         """Block-level parity probe (sepvad_set_tcn_dump): one forward of x with the fused TCN, returning
