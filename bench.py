@@ -324,7 +324,8 @@ def main():
                     help="offline: cfg 2 (default, the BASELINE metric: B=64, N=32000); cfg4: 8 s reverberant "
                          "mixtures, B=64/GPU, N=64000 (T=251); cfg5: B=128/GPU, N=32000 (run with --precision "
                          "f16 for the fp16 arm); long: 16 s files as only_inference.py forwards them (B=8/GPU, "
-                         "N=256000, T=1001: fused groups of 32 workgroups); stream: cfg 3 streaming wrapper")
+                         "N=256000, T=1001: fused groups of 32 workgroups; --samples 480000 --batch 4 for 30 s files, groups of 59 "
+                         "spanning XCDs); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
     rc = launch_ranks(args)
     if rc is not None:
@@ -449,7 +450,7 @@ def main():
                              "cfg5": f"cfg5 config_with_vad.json forward, B={B}/GPU, N={N} samples, T={T} "
                                      f"frames, {args.precision} GEMMs",
                              "long": f"long files (only_inference.py:90-91 forwards a whole file), config_with_vad.json, "
-                                     f"B={B}/GPU, N={N} samples (16 s @ 16 kHz), T={T} frames"}[args.workload]
+                                     f"B={B}/GPU, N={N} samples ({N / 16000:.1f} s @ 16 kHz), T={T} frames"}[args.workload]
                             + "; full forward: STFT, 24 TCN blocks, VAD, iSTFT, est (side attributes on read)",
                 "global_batch": world * B,
                 "seq_len": N,

@@ -49,6 +49,7 @@ struct PackedW {
   size_t w32 = 0, whi = 0, wlo = 0, scale = 0;
   size_t fhi = 0, flo = 0;  // fused-TCN copies in MFMA B-fragment order (see pack_pointwise)
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
+  size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
 };
 
 struct BlockOff {
@@ -145,11 +146,14 @@ struct sepvad_model {
   int split = 1;
   hipStream_t sub[MAX_SPLIT] = {};
   hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
-  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs are not fp32 and T <= 1024
+  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs are not fp32 and T <= 4096
   bool fused = true;
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU), max over precisions
   int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
-  __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered fp16 hi/lo weights (F16X3)
+  __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered fp16 hi/lo weights (F16X3, SEPVAD_WLO_F16)
+  __half* twq = nullptr;        // [nblk][WQ_BLOCK] fragment-ordered fp16 hi + e4m3 lo weights (F16X3, SEPVAD_WLO_E4M3)
+  int lo8 = 0;                  // k_tcn's weight lo plane: fp16 (0, default) or e4m3 (1); SEPVAD_WLO / sepvad_set_weight_lo
+  int tcn_cap_q = 0;            // co-resident capacity of the e4m3-lo k_tcn
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
@@ -238,6 +242,28 @@ __half bf16_bits(float f) {
   return h;
 }
 
+// float -> e4m3fn (OCP FP8: 1-4-3, bias 7, max 448 = 0x7e, 0x7f NaN, no inf): round to nearest even, saturating.
+// The gfx950 conversions (v_cvt_scalef32_pk_f16_fp8) read the same OCP format.
+}  // namespace
+uint8_t sepvad::e4m3_rn(float x) {
+  if (std::isnan(x)) return 0x7f;
+  const uint8_t sg = std::signbit(x) ? 0x80 : 0x00;
+  const double a = std::fabs((double)x);
+  if (a >= 448.0) return sg | 0x7e;
+  if (a < std::ldexp(1.0, -6)) {                       // subnormal range: m * 2^-9, m = 0..8 (8 = smallest normal)
+    const int m = (int)std::nearbyint(std::ldexp(a, 9));  // the default rounding mode: to nearest even
+    return sg | (uint8_t)m;
+  }
+  int k = 0;
+  (void)std::frexp(a, &k);                             // a = f * 2^k, f in [0.5, 1): exponent E = k - 1
+  int E = k - 1;
+  int q = (int)std::nearbyint(std::ldexp(a, 3 - E));   // 8..16
+  if (q == 16) { q = 8; ++E; }
+  if (E > 8 || (E == 8 && q > 14)) return sg | 0x7e;   // rounded past 448: saturate
+  return sg | (uint8_t)(((E + 7) << 3) | (q - 8));
+}
+namespace {
+
 // [cout][cin] fp32 -> zero-padded [mpad][cin] fp32 + the fp16 hi/lo split of each row scaled by
 // 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^(e + col_e) undoes it exactly, and
 // also the 2^-col_e the GEMM applies to its A operand before splitting it (range guard, see range_exp).
@@ -245,6 +271,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   PackedW p;
   std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
   std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin), bf((size_t)mpad * cin);
+  std::vector<float> lo32((size_t)mpad * cin);  // the exact fp32 residual (source of the e4m3 lo plane)
   for (int o = 0; o < mpad; ++o) {
     float mx = 0.f;
     if (o < cout)
@@ -259,7 +286,8 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
       const float vs = v * s;
       const __half hh = __float2half_rn(vs);
       hi[(size_t)o * cin + i] = hh;
-      lo[(size_t)o * cin + i] = __float2half_rn(vs - __half2float(hh));
+      lo32[(size_t)o * cin + i] = vs - __half2float(hh);
+      lo[(size_t)o * cin + i] = __float2half_rn(lo32[(size_t)o * cin + i]);
       bf[(size_t)o * cin + i] = bf16_bits(vs);
     }
   }
@@ -286,6 +314,22 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
     p.fhi = pk.addh(fh);
     p.flo = pk.addh(fl);
     p.fbf = pk.addh(fb);
+    // e4m3 lo plane: lane l, K-step pair pr -> 16 bytes: j = 0..7 of step 2 pr, then of step 2 pr + 1
+    if ((cin / 16) % 2 == 0) {
+      std::vector<uint8_t> f8((size_t)mpad * cin);
+      size_t b = 0;
+      for (int mt = 0; mt < mpad / 32; ++mt)
+        for (int pr = 0; pr < cin / 32; ++pr)
+          for (int l = 0; l < 64; ++l)
+            for (int h = 0; h < 2; ++h)
+              for (int j = 0; j < 8; ++j, ++b) {
+                const size_t src = (size_t)(32 * mt + (l & 31)) * cin + 16 * (2 * pr + h) + 8 * (l >> 5) + j;
+                f8[b] = e4m3_rn(lo32[src] * (float)(1 << WQ_LO_SHIFT));  // exact power-of-two scaling
+              }
+      std::vector<__half> f8h(f8.size() / 2);
+      std::memcpy(f8h.data(), f8.data(), f8.size());
+      p.fl8 = pk.addh(f8h);
+    }
   }
   return p;
 }
@@ -415,11 +459,13 @@ int init_fused(sepvad_model* h, const Packer& pk) {
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
   for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
     // co-resident workgroups of the persistent TCN kernel that will run (both use one 512-thread workgroup per CU)
-    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p);
+    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, false);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
   }
+  h->tcn_cap_q = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, true);
+  h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q);
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
-  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk);
+  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
   for (int i = 0; i < h->nblk; ++i) {
@@ -429,6 +475,11 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     std::copy_n(pk.hblob.begin() + bo.w1.flo, WF_W1L, w + WF_W1L);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WF_W2L - WF_W2H, w + WF_W2H);
     std::copy_n(pk.hblob.begin() + bo.w2.flo, WF_W2L - WF_W2H, w + WF_W2L);
+    __half* wqb = wq.data() + WQ_BLOCK * i;
+    std::copy_n(pk.hblob.begin() + bo.w1.fhi, WQ_W1L, wqb);
+    std::copy_n(pk.hblob.begin() + bo.w1.fl8, WQ_W2H - WQ_W1L, wqb + WQ_W1L);
+    std::copy_n(pk.hblob.begin() + bo.w2.fhi, WQ_W2L - WQ_W2H, wqb + WQ_W2H);
+    std::copy_n(pk.hblob.begin() + bo.w2.fl8, WQ_BLOCK - WQ_W2L, wqb + WQ_W2L);
     std::copy_n(pk.hblob.begin() + bo.w1.fhi, WS_W2, ws16.data() + WS_BLOCK * i);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WS_BLOCK - WS_W2, ws16.data() + WS_BLOCK * i + WS_W2);
     std::copy_n(pk.hblob.begin() + bo.w1.fbf, WS_W2, wsbf.data() + WS_BLOCK * i);
@@ -457,6 +508,8 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   }
   HIPCHK(hipMalloc(&h->twf, wf.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twq, wq.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twq, wq.data(), wq.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twf16, ws16.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf16, ws16.data(), ws16.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twbf, wsbf.size() * sizeof(__half)));
@@ -802,6 +855,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     return nullptr;
   }
   if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
+  if (const char* wl = getenv("SEPVAD_WLO")) h->lo8 = std::strcmp(wl, "e4m3") == 0;  // "f16" (default) | "e4m3"
   if (init_fused(h, pk) != SEPVAD_OK) {
     sepvad_destroy(h);
     return nullptr;
@@ -828,6 +882,19 @@ int32_t sepvad_set_precision(sepvad_handle h, int32_t precision) {
   return SEPVAD_OK;
 }
 
+int32_t sepvad_set_weight_lo(sepvad_handle h, int32_t mode) {
+  if (!h) return fail(SEPVAD_E_ARG, "null handle");
+  if (mode != SEPVAD_WLO_E4M3 && mode != SEPVAD_WLO_F16) return fail(SEPVAD_E_ARG, "unknown weight lo-plane format");
+  h->lo8 = mode == SEPVAD_WLO_E4M3;
+  return SEPVAD_OK;
+}
+
+int32_t sepvad_e4m3_encode(const float* in, uint8_t* out, int64_t n) {
+  if ((!in || !out) && n > 0) return fail(SEPVAD_E_ARG, "sepvad_e4m3_encode: null buffer");
+  for (int64_t i = 0; i < n; ++i) out[i] = e4m3_rn(in[i]);
+  return SEPVAD_OK;
+}
+
 int32_t sepvad_set_timing(sepvad_handle h, int32_t on) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
   h->timing = on != 0;
@@ -846,14 +913,19 @@ int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, 
 
 namespace {
 
-// The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 32 * FG_MAX = 1024) and a group fits
+// The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 32 * FG_MAX = 4096) and a group fits
 // the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
 static_assert(SEPVAD_PREC_FP32 == PREC_F32 && SEPVAD_PREC_F16X3 == PREC_F16X3 && SEPVAD_PREC_F16 == PREC_F16 &&
               SEPVAD_PREC_BF16 == PREC_BF16, "precision codes");
 
+// co-resident k_tcn workgroups of the variant that will run (the e4m3-lo kernel is its own instantiation)
+int tcn_cap_of(const sepvad_model* h) {
+  return h->prec == PREC_F16X3 && h->lo8 ? h->tcn_cap_q : h->tcn_cap_p[h->prec];
+}
+
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && h->tcn_cap_p[h->prec] >= G;
+  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G;
 }
 
 int env_int(const char* name, int dflt) {
@@ -975,7 +1047,8 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
     ta.prec = h->prec;
-    ta.wfrag = h->prec == PREC_F16X3 ? h->twf : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
+    ta.lo8 = h->prec == PREC_F16X3 && h->lo8;
+    ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
     ta.prm = h->tprm;
     ta.inv_ch = 1.0 / ((double)CH * T);
     ta.inv_hid = 1.0 / ((double)HID * T);
@@ -985,7 +1058,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     auto launch_t = [&](const TcnArgs& t, int grid) { return launch_tcn(t, grid, s); };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
-    int ngroups = std::min(B, h->tcn_cap_p[h->prec] / G);
+    int ngroups = std::min(B, tcn_cap_of(h) / G);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
     // counted as 4 (headroom)
@@ -1662,6 +1735,7 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->fork) (void)hipEventDestroy(h->fork);
   for (auto& c : h->ctx) free_ctx(c.release());
   if (h->twf) (void)hipFree(h->twf);
+  if (h->twq) (void)hipFree(h->twq);
   if (h->twf16) (void)hipFree(h->twf16);
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);

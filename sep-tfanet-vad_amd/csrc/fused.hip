@@ -88,6 +88,15 @@ constexpr int HROW = FR + 8;      // conv1d output rows incl. 4 halo rows on eac
 #define TCN_PD 8     // weight K steps in flight per wave (4: +10 us; 16: spills at 2 waves per SIMD)
 #endif
 constexpr int PD = TCN_PD;        // weight K steps in flight per wave
+#ifndef TCN_DIAG
+#define TCN_DIAG 0   // diagnostics only (wrong results): 1 = GEMM ring refills skipped, 2 = GEMM MFMAs skipped
+#endif
+#ifndef TCN_AD
+#define TCN_AD 1     // GEMM A-fragment LDS reads issued this many K steps ahead (2: no gain, profiles/r03h_ab_*)
+#endif
+#ifndef TCN_PDQ
+#define TCN_PDQ 8    // ... with the e4m3 lo plane (16 fits the registers, 238 VGPRs, but measured 4 % more cycles)
+#endif
 constexpr int NS1 = CH / 16;      // conv1d K steps (256 / 16)
 constexpr int NS2 = HID / 16;     // res_out K steps (512 / 16)
 
@@ -120,11 +129,12 @@ constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
 static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
-template <int PRE>
+template <int PRE, bool L8 = false>
 struct WLay {
-  static constexpr size_t BLOCK = PRE == PREC_F16X3 ? WF_BLOCK : WS_BLOCK;
-  static constexpr size_t W1H = 0, W1L = PRE == PREC_F16X3 ? WF_W1L : 0;
-  static constexpr size_t W2H = PRE == PREC_F16X3 ? WF_W2H : WS_W2, W2L = PRE == PREC_F16X3 ? WF_W2L : 0;
+  static constexpr bool X3 = PRE == PREC_F16X3;
+  static constexpr size_t BLOCK = X3 ? (L8 ? WQ_BLOCK : WF_BLOCK) : WS_BLOCK;
+  static constexpr size_t W1H = 0, W1L = X3 ? (L8 ? WQ_W1L : WF_W1L) : 0;
+  static constexpr size_t W2H = X3 ? (L8 ? WQ_W2H : WF_W2H) : WS_W2, W2L = X3 ? (L8 ? WQ_W2L : WF_W2L) : 0;
 };
 
 // conv1d / res_out GEMM of one wave: acc[32 frames x 32 channels] += A[32 x 16*NS] * W^T. A comes from
@@ -133,14 +143,31 @@ struct WLay {
 // static register ring; the first PD steps are already in (rh, rl) on entry.
 // PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
 // hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
-template <int NS, int LDA, int PRE, int RD = PD>
+// L8 (F16X3 only): the lo plane is e4m3 (sepvad_internal.h WQ_*), one 1 KB wave load per two K steps at
+// voffl + 1024 * pair into rl[i / 2], widened to fp16 in registers (v_cvt_scalef32_pk_f16_fp8, 4 per step,
+// scale 2^-WQ_LO_SHIFT) right before the step's MFMAs: 3 bytes per weight instead of 4.
+__device__ __forceinline__ f16x8 lo8_widen(u32x4v q, int half) {
+  constexpr float sc = 1.0f / (float)(1 << WQ_LO_SHIFT);
+  const unsigned d0 = half ? q[2] : q[0], d1 = half ? q[3] : q[1];
+  const h16x2 c0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, false);
+  const h16x2 c1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, true);
+  const h16x2 c2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, false);
+  const h16x2 c3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, true);
+  return f16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
+}
+
+template <int NS, int LDA, int PRE, int RD = PD, bool L8 = false>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
-                                          __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
+                                          __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
   static_assert(NS % RD == 0 && NS >= RD, "K steps");
+  static_assert(!L8 || (PRE == PREC_F16X3 && RD % 2 == 0), "e4m3 lo plane: F16X3, K-step pairs");
   constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
-  // A fragments one step ahead: the LDS reads of step s+1 are in flight during step s's MFMAs
+  // A fragments AD steps ahead: the LDS reads of step s+AD are in flight during steps s..s+AD-1 (AD = 2: a wave that
+  // has the SIMD's matrix pipe to itself -- the other wave of the SIMD done with its GEMM -- issues a step every ~96
+  // cycles, shorter than an LDS read under load)
+#if TCN_AD == 0  // round-2 form (one step ahead, copies)
   f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff);
   f16x8 al = ah;
   if constexpr (X3) al = *reinterpret_cast<const f16x8*>(Alo + aoff);
@@ -150,9 +177,31 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
       if constexpr (X3) nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
     }
-    if constexpr (X3) {
+    constexpr int AD = 1;
+#else
+  constexpr int AD = TCN_AD;
+  f16x8 aH[AD + 1], aL[AD + 1];
+#pragma unroll
+  for (int k = 0; k < AD; ++k) {
+    aH[k] = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * k);
+    aL[k] = aH[k];
+    if constexpr (X3) aL[k] = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * k);
+  }
+  auto step = [&](int s, int i, bool pf) {
+    const int cur = s % (AD + 1), nxt = (s + AD) % (AD + 1);
+    if (s + AD < NS) {
+      aH[nxt] = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + AD));
+      if constexpr (X3) aL[nxt] = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + AD));
+    }
+    const f16x8 ah = aH[cur], al = aL[cur];
+#endif
+    if constexpr (TCN_DIAG == 2) {
+      acc[0] += (float)ah[0] + (float)al[0] + __builtin_bit_cast(float, rh[i][0]) + __builtin_bit_cast(float, rl[i][0]);
+    } else if constexpr (X3) {
       const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
-      const f16x8 bl = __builtin_bit_cast(f16x8, rl[i]);
+      f16x8 bl;
+      if constexpr (L8) bl = lo8_widen(rl[i >> 1], i & 1);
+      else bl = __builtin_bit_cast(f16x8, rl[i]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
@@ -162,15 +211,22 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, rh[i]),
                                                     acc, 0, 0, 0);
     }
-    if (pf) {
-      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
-      if constexpr (X3) rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
+    // ring refill: hi entry i every step; the lo pair i/2 once both of its steps are consumed (odd i)
+    if (TCN_DIAG == 1) pf = false;
+    const bool pfl = pf && X3 && (!L8 || (i & 1));
+    if (pf) rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (s + RD) * 1024, 0);
+    if (pfl) {
+      if constexpr (L8) rl[i >> 1] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, ((s + RD) >> 1) * 1024, 0);
+      else rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
     }
+#if TCN_AD == 0
     ah = nh; al = nl;
-    // pipeline shape of a step: next step's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
-    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
+#endif
+    // pipeline shape of a step: step s+AD's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
+    if (s + AD < NS) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 : 1, 0);
-    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, X3 ? 2 : 1, 0);
+    if (pfl) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+    else if (pf) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     // keep program order per step: the scheduler otherwise may sink the refill loads to their use and
     // collapse the ring to one step in flight (seen as s_waitcnt vmcnt(1) before every step)
     __builtin_amdgcn_sched_barrier(0);
@@ -184,23 +240,31 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
 }
 
-template <int PRE, int RD = PD>
-__device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
+template <int PRE, int RD = PD, bool L8 = false>
+__device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD]) {
 #pragma unroll
   for (int s = 0; s < RD; ++s) {
     rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
-    if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+    if constexpr (L8) {
+      if (s % 2 == 0) rl[s / 2] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, (s / 2) * 1024, 0);
+    } else if constexpr (PRE == PREC_F16X3) {
+      rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+    }
   }
 }
 
 // Ring entry s only (the burst above spread over a phase's rows: a CU's texture path takes one 1 KB wave load
 // per ~16 clocks, so 8 waves issuing the whole ring at once stall ~1 us on issue)
-template <int PRE>
-__device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff,
-                                            u32x4v (&rh)[PD], u32x4v (&rl)[PD], int s) {
+template <int PRE, int RD, bool L8 = false>
+__device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
+                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD], int s) {
   rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
-  if constexpr (PRE == PREC_F16X3) rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+  if constexpr (L8) {
+    if (s % 2 == 0) rl[s / 2] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, (s / 2) * 1024, 0);
+  } else if constexpr (PRE == PREC_F16X3) {
+    rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
+  }
 }
 
 // GroupNorm affine of the 256 channels, one per thread tid < CH (as device_common.h gn_affine); the
@@ -276,9 +340,12 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   }
 }
 
-template <int LM, int PRE, bool DUMP = false>
+template <int LM, int PRE, bool DUMP = false, bool L8 = false>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
-  using WL = WLay<PRE>;
+  using WL = WLay<PRE, L8>;
+  constexpr int RD = L8 ? TCN_PDQ : PD;  // weight K steps in flight per wave
+  constexpr int RPI = RD / 8;            // ring entries issued per row of the phases before the GEMMs (8 row steps)
+  static_assert(RD % 8 == 0 && RD <= 16, "ring depth: 8 or 16 K steps");
   __shared__ __attribute__((aligned(16))) TcnSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
@@ -320,6 +387,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
   const int voff1 = (wave * NS1 * 64 + lane) * 16, voff2 = (wave * NS2 * 64 + lane) * 16;
+  // ... and of its 16-B lo fragment pair (e4m3 lo plane: one 1 KB wave load per two K steps)
+  const int voff1l = (wave * (NS1 / 2) * 64 + lane) * 16, voff2l = (wave * (NS2 / 2) * 64 + lane) * 16;
 
   for (int u = grp; u < a.B; u += ngroups) {
     // opaque per-utterance copies (as in the block loop): keeps hipcc from hoisting and spilling the
@@ -330,7 +399,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     // The first-touch loads of the input (S0 rows, LN parameters, the LN records) are issued before
     // anything waits, so their latencies overlap.
     float o[16];
-    u32x4v rh[PD], rl[PD];
+    u32x4v rh[RD], rl[RD];
     {
     const int m = mu_, tid = tidu;
     auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4u; };
@@ -345,7 +414,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const __amdgpu_buffer_rsrc_t gr = rsrc_of(ka->ln.g), ber = rsrc_of(ka->ln.be);
       const __amdgpu_buffer_rsrc_t w1h = rsrc_of(ka->wfrag), w1l = rsrc_of(ka->wfrag + WL::W1L);
       const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
-      const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * 16;
+      const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * 16, voffu_l = (wave_s * (NS1 / 2) * 64 + (tid & 63)) * 16;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 16; ++r)  // rows < G*32 <= Tp: in bounds (masked below)
@@ -355,7 +424,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
       sx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc_of(ka->prm), 0, PB_SX * 4, 0));
-      prefetch_w<PRE>(w1h, w1l, voffu, rh, rl);  // block-0 conv1d weights: in flight with the input rows
+      prefetch_w<PRE, RD, L8>(w1h, w1l, voffu, voffu_l, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
     if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
@@ -442,7 +511,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS1, LDX, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, rh, rl, lane);
+        wave_gemm<NS1, LDX, PRE, RD, L8>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, voff1l, rh, rl, lane);
       TPROBE(1);
       }
       {
@@ -546,7 +615,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        if (!TCN_PFX) prefetch_w<PRE>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl);
+        if (!TCN_PFX) prefetch_w<PRE, RD, L8>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
@@ -600,7 +669,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
 #pragma unroll
           for (int i = 0; i < FR / 4; ++i) {
-            if (TCN_PFX && i < PD) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i);  // res_out ring entry i
+#pragma unroll
+            for (int e = 0; e < RPI; ++e)  // res_out ring entries RPI i .. RPI i + RPI - 1
+              if (TCN_PFX) prefetch_w1<PRE, RD, L8>(w2h, w2l, voff2, voff2l, rh, rl, RPI * i + e);
             const int tl = fr0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;
             f32x2 y[2];
@@ -616,7 +687,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             store_d4<PRE>(sm.Ahi + tl * LDD + 2 * c2, sm.Alo + tl * LDD + 2 * c2, y[0], y[1]);
           }
         };
-        static_assert(PD <= FR / 4, "one ring entry per frame of the packed depthwise conv");
+        static_assert(RD == RPI * FR / 4, "RPI ring entries per frame of the packed depthwise conv");
 #else
         const float sc = rs * pm[PB_G1 + c], sh = pm[PB_BE1 + c] - sc * mu;
         float wv[2][4];
@@ -643,7 +714,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
-            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE>(w2h, w2l, voff2, rh, rl, i / 2);
+            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE, RD, L8>(w2h, w2l, voff2, voff2l, rh, rl, i / 2);
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -682,7 +753,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS2, LDD, PRE>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, rh, rl, lane);
+        wave_gemm<NS2, LDD, PRE, RD, L8>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl,
+                                         lane);
       TPROBE(5);
       }
 #if TCN_M23
@@ -758,10 +830,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             const int tl = mi - 4, t = t0 + tl;
             if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
           }
-          const int kq = tid - (NTHR - 128);  // threads 384..: GN2 word kq of the 4G (wave 6 holds all of them for G <= 16)
-          const u64* pq = (kq >= 0 && kq < 4 * G) ? slot(kq >> 2, e2) + GW_STAT + (kq & 3) : nullptr;
+          // threads 384..: GN2 words kq + 128 j (j < 4) of the 4G (wave 6 holds all of them for G <= 16; up to 128
+          // members, 512 words, in the first pass's free slots)
+          const int kq = tid - (NTHR - 128);
           float s = 0.f, vat = 0.f;
-          unsigned vq = 0u;
+          unsigned vq[4] = {0u, 0u, 0u, 0u};
           for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
 #pragma unroll
             for (int mm = 0; mm < FG_CHUNK; ++mm) {
@@ -769,23 +842,41 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               tg[mm] = tag3;
             }
             if (c0 == 0 && mi >= 0) pp[0] = pat;
-            if (c0 == 0 && kq >= 0) { pp[0] = pq; tg[0] = tag2; }
+            if (c0 == 0 && kq >= 0) {
+              if (G <= 32) {
+                pp[0] = kq < 4 * G ? slot(kq >> 2, e2) + GW_STAT + (kq & 3) : nullptr;
+                tg[0] = tag2;
+              } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const int w = kq + 128 * j;
+                  pp[j] = w < 4 * G ? slot(w >> 2, e2) + GW_STAT + (w & 3) : nullptr;
+                  tg[j] = tag2;
+                }
+              }
+            }
             gpollt<FG_CHUNK>(pp, tg, v, a);
             if (tid < CH) {
 #pragma unroll
               for (int mm = 0; mm < FG_CHUNK; ++mm)
                 if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
-            if (c0 == 0) { vat = __builtin_bit_cast(float, v[0]); vq = v[0]; }
+            if (c0 == 0) {
+              vat = __builtin_bit_cast(float, v[0]);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) vq[j] = v[j];
+            }
           }
           if (G <= FG_WAVE) {
             if (wave_s == 6) {
               float mu, rs;
-              member_moments_w(vq, 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
+              member_moments_w(vq[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
               if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
             }
-          } else if (kq >= 0 && kq < 4 * G) {
-            sm.gw[kq] = vq;
+          } else if (kq >= 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (kq + 128 * j < 4 * G) sm.gw[kq + 128 * j] = vq[j];
           }
           __syncthreads();  // csum, the GN2 moments / words complete
           float fmu, frs;
@@ -1044,16 +1135,28 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
         if (tid < NMOM) gputd(slot(g, e4) + GW_STAT + 2 * tid, tag4, sm.dred[tid], l2);
         {
-          const int k = tid;  // word k % 22 of member k / 22
-          const u64* pp[1] = {k < 2 * NMOM * G ? slot(k / (2 * NMOM), e4) + GW_STAT + k % (2 * NMOM) : nullptr};
-          unsigned v[1];
-          gpoll<1>(pp, tag4, v, a);
-          if (k < 2 * NMOM * G) sm.gw[k] = v[0];
-          if (2 * NMOM * G > NTHR) {  // more than 23 members: the remaining words in a second pass
-            const int k2 = tid + NTHR;
-            const u64* p2[1] = {k2 < 2 * NMOM * G ? slot(k2 / (2 * NMOM), e4) + GW_STAT + k2 % (2 * NMOM) : nullptr};
-            gpoll<1>(p2, tag4, v, a);
-            if (k2 < 2 * NMOM * G) sm.gw[k2] = v[0];
+          // word k % 22 of member k / 22: one word per thread up to 23 members; beyond, passes of up to four words in
+          // flight per thread (128 members: 2816 words, two passes)
+          const int nw = 2 * NMOM * G;
+          if (nw <= NTHR) {
+            const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_STAT + tid % (2 * NMOM) : nullptr};
+            unsigned v[1];
+            gpoll<1>(pp, tag4, v, a);
+            if (tid < nw) sm.gw[tid] = v[0];
+          } else for (int k0 = 0; k0 < nw; k0 += 4 * NTHR) {
+            const u64* pp[4];
+            unsigned v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int k = k0 + tid + j * NTHR;
+              pp[j] = k < nw ? slot(k / (2 * NMOM), e4) + GW_STAT + k % (2 * NMOM) : nullptr;
+            }
+            gpoll<4>(pp, tag4, v, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int k = k0 + tid + j * NTHR;
+              if (k < nw) sm.gw[k] = v[j];
+            }
           }
         }
       TPROBE(11);
@@ -1097,7 +1200,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
       const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
       const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
-      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE>(wnh, wnl, voff1, rh, rl);
+      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl);
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
@@ -1105,7 +1208,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #if TCN_PKE
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          if (TCN_PFX) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
+#pragma unroll
+          for (int e = 0; e < RPI; ++e)
+            if (TCN_PFX) prefetch_w1<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl, RPI * (r / 2) + e);
           const int tl = trow(r);
           const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r], rv[r + 1]}, kc);  // rv gated above
           const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
@@ -1116,7 +1221,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE>(wnh, wnl, voff1, rh, rl, r / 2);
+          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
@@ -1244,12 +1349,12 @@ __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
   const int voff = (j * NS1 * 64 + lane) * 16;
   constexpr int HRD = 4;  // ring depth (k_tcn uses PD = 8 at 2 waves per SIMD)
   u32x4v rh[HRD], rl[HRD];
-  prefetch_w<PRE, HRD>(wh, wl, voff, rh, rl);
+  prefetch_w<PRE, HRD>(wh, wl, voff, 0, rh, rl);
   const int hl4 = 4 * (lane >> 5);
   f32x16v acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  wave_gemm<NS1, LDX, PRE, HRD>(acc, Ahi, Alo, wh, wl, voff, rh, rl, lane);
+  wave_gemm<NS1, LDX, PRE, HRD>(acc, Ahi, Alo, wh, wl, voff, 0, rh, rl, lane);
   stamp(4);
   // the VAD GEMM's B fragments (this wave's two K steps, hi and lo), in flight during the mask stores
   f16x8 vb[2][2];
@@ -1333,23 +1438,23 @@ hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int PRE>
+template <int PRE, bool L8>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
   if constexpr (PRE == PREC_F16X3) {
     if (a.dump != nullptr) {  // parity-probe instantiation (the probe code stays out of the production kernels)
       switch (a.ln_mode) {
-        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
     }
   }
   switch (a.ln_mode) {
-    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1359,30 +1464,30 @@ hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
   if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || grid < a.G || grid % a.G)
     return hipErrorInvalidValue;
   switch (a.prec) {
-    case PREC_F16X3: return launch_tcn_pre<PREC_F16X3>(a, grid, s);
-    case PREC_F16: return launch_tcn_pre<PREC_F16>(a, grid, s);
-    case PREC_BF16: return launch_tcn_pre<PREC_BF16>(a, grid, s);
+    case PREC_F16X3: return a.lo8 ? launch_tcn_pre<PREC_F16X3, true>(a, grid, s) : launch_tcn_pre<PREC_F16X3, false>(a, grid, s);
+    case PREC_F16: return launch_tcn_pre<PREC_F16, false>(a, grid, s);
+    case PREC_BF16: return launch_tcn_pre<PREC_BF16, false>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }
 
-template <int PRE>
+template <int PRE, bool L8>
 static int blocks_per_cu_pre(int ln_mode) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
   switch (ln_mode) {
-    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE, PRE>, NTHR, 0); break;
-    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE>, NTHR, 0); break;
-    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE>, NTHR, 0); break;
+    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE, PRE, false, L8>, NTHR, 0); break;
+    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE, false, L8>, NTHR, 0); break;
+    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE, false, L8>, NTHR, 0); break;
   }
   return e == hipSuccess ? nb : 0;
 }
 
-int tcn_blocks_per_cu(int ln_mode, int prec) {
+int tcn_blocks_per_cu(int ln_mode, int prec, bool lo8) {
   switch (prec) {
-    case PREC_F16X3: return blocks_per_cu_pre<PREC_F16X3>(ln_mode);
-    case PREC_F16: return blocks_per_cu_pre<PREC_F16>(ln_mode);
-    case PREC_BF16: return blocks_per_cu_pre<PREC_BF16>(ln_mode);
+    case PREC_F16X3: return lo8 ? blocks_per_cu_pre<PREC_F16X3, true>(ln_mode) : blocks_per_cu_pre<PREC_F16X3, false>(ln_mode);
+    case PREC_F16: return blocks_per_cu_pre<PREC_F16, false>(ln_mode);
+    case PREC_BF16: return blocks_per_cu_pre<PREC_BF16, false>(ln_mode);
   }
   return 0;
 }

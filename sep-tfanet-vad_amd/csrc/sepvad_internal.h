@@ -276,7 +276,11 @@ hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
 // ---- fused persistent TCN (fused.hip) ----
 constexpr int FR = 32;          // frames per workgroup
-constexpr int FG_MAX = 32;      // workgroups per utterance (T <= 1024: 16.4 s at 16 kHz in one fused forward)
+#ifndef SEPVAD_FG_MAX
+#define SEPVAD_FG_MAX 128
+#endif
+constexpr int FG_MAX = SEPVAD_FG_MAX;  // workgroups per utterance (T <= 4096: 65.5 s at 16 kHz in one fused forward; groups
+                                // above 32 members span XCDs and hand off through write-through words)
 constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
 constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
 constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
@@ -297,9 +301,17 @@ constexpr int PB_SIZE = 4904;                                      // multiple o
 constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
 // single-plane (PREC_F16 / PREC_BF16) blobs: conv1d (256x256) | res_out (256x512)
 constexpr size_t WS_W2 = 65536, WS_BLOCK = 196608;  // halves
+// F16X3 with an e4m3 lo plane (k_tcn default, SEPVAD_WLO_E4M3): conv1d hi (256x256 halves) | conv1d lo (256x256
+// bytes) | res_out hi (256x512 halves) | res_out lo (bytes). A lo byte is e4m3fn(lo * 2^WQ_LO_SHIFT): |lo| <= 2^-12 of
+// the row-scaled weight, so the stored value is <= 2^7 (e4m3 max 448) and keeps 4 significant bits down to 2^-25.
+// Lo fragment order: [row tile][K-step PAIR][64 lanes][16 bytes: 8 of step 2p, 8 of step 2p+1] (one 1 KB wave load
+// per two K steps; the hi plane keeps one per step).
+constexpr size_t WQ_W1L = 65536, WQ_W2H = 98304, WQ_W2L = 229376, WQ_BLOCK = 294912;  // halves
+constexpr int WQ_LO_SHIFT = 19;
 struct TcnArgs {
   int B, T, Tp, G, nblk, layer, ln_mode, tf_att, prec;
-  const __half* wfrag;   // [nblk][WF_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
+  int lo8;               // F16X3: the weight lo plane is e4m3 (WQ_* layout) instead of fp16 (WF_*)
+  const __half* wfrag;   // [nblk][WF_BLOCK | WQ_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
   const float* prm;      // [nblk][PB_SIZE] parameter blobs
   const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
   GnSrc ln;              // TCN.LN statistics records (k_gate) + affine
@@ -343,7 +355,9 @@ struct HeadArgs {
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_head(const HeadArgs& a, hipStream_t s);
-int tcn_blocks_per_cu(int ln_mode, int prec);
+int tcn_blocks_per_cu(int ln_mode, int prec, bool lo8);
+// host: float -> e4m3fn (OCP FP8, bias 7, max 448, no inf), round to nearest even, saturating
+uint8_t e4m3_rn(float x);
 
 hipError_t launch_gemm(const GemmArgs& a, int ep, hipStream_t s);
 hipError_t launch_dw_stats(const DwStatsArgs& a, hipStream_t s);

@@ -9,6 +9,7 @@ namespace sepvad {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 

@@ -160,6 +160,9 @@ class SeparationModel(nn.Module):
         # GEMM arithmetic of the native path: "f16x3" (fp32-equivalent split on fp16 MFMA, default)
         # or "fp32" (fp32 MFMA); both meet the fp32 parity gates. SEPVAD_PRECISION overrides.
         self.native_precision = os.environ.get("SEPVAD_PRECISION", "f16x3")
+        # storage of the f16x3 weight lo plane in the fused TCN: "f16" (default) or "e4m3" (opt-in, 3 B per weight
+        # streamed; include/sepvad.h SEPVAD_WLO_*); SEPVAD_WLO overrides
+        self.native_weight_lo = os.environ.get("SEPVAD_WLO", "f16")
 
     # -- native handle -------------------------------------------------------------------------
     # The handle (folded, packed device weights) is rebuilt lazily after load_state_dict(),
@@ -187,6 +190,8 @@ class SeparationModel(nn.Module):
             self._handles[device] = h
         elif h.precision != self.native_precision:
             h.set_precision(self.native_precision)
+        if getattr(h, "weight_lo", None) != self.native_weight_lo:
+            h.set_weight_lo(self.native_weight_lo)
         return h
 
     # -- side attributes (model/model.py:412,421,429), materialised on first read ---------------------

@@ -19,9 +19,12 @@ SEPVAD_LN_PLAIN, SEPVAD_LN_RECURSIVE, SEPVAD_LN_RESIDUAL = 0, 1, 2
 SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3, SEPVAD_PREC_F16, SEPVAD_PREC_BF16 = 0, 1, 2, 3
 # fp32 / f16x3: fp32-equivalent (parity path); f16 / bf16: reduced-precision arms (tolerance measured)
 PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVAD_PREC_F16, "bf16": SEPVAD_PREC_BF16}
+# storage of the f16x3 weight lo plane in the fused TCN (include/sepvad.h SEPVAD_WLO_*)
+WEIGHT_LO = {"e4m3": 0, "f16": 1}
 
 EXPORTED_SYMBOLS = (
-    "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_forward", "sepvad_forward_strided",
+    "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_set_weight_lo", "sepvad_e4m3_encode",
+    "sepvad_forward", "sepvad_forward_strided",
     "sepvad_forward_windows", "sepvad_pit_l1_sums", "sepvad_pit_l1_choose",
     "sepvad_set_split", "sepvad_set_fused", "sepvad_fused_status", "sepvad_side_outputs", "sepvad_set_tcn_dump",
     "sepvad_last_forward", "sepvad_side_outputs_of", "sepvad_release_stream", "sepvad_tcn_clock",
@@ -77,6 +80,10 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_reserve.argtypes = [P, i32, i32]
     lib.sepvad_set_precision.restype = i32
     lib.sepvad_set_precision.argtypes = [P, i32]
+    lib.sepvad_set_weight_lo.restype = i32
+    lib.sepvad_set_weight_lo.argtypes = [P, i32]
+    lib.sepvad_e4m3_encode.restype = i32
+    lib.sepvad_e4m3_encode.argtypes = [P, P, ctypes.c_int64]
     lib.sepvad_forward.restype = i32
     lib.sepvad_forward.argtypes = [P, P, i32, i32, ctypes.POINTER(SepVadOutputs), ctypes.POINTER(SepVadInferKw), P]
     lib.sepvad_forward_strided.restype = i32
@@ -229,6 +236,11 @@ class Handle:
     def set_precision(self, precision: str):
         _check(self._lib.sepvad_set_precision(self._h, PRECISIONS[precision]), "sepvad_set_precision")
         self.precision = precision
+
+    def set_weight_lo(self, mode: str):
+        """Weight lo plane of the fused TCN's f16x3 GEMMs: "f16" (default) or "e4m3" (opt-in, 3 B per weight)."""
+        _check(self._lib.sepvad_set_weight_lo(self._h, WEIGHT_LO[mode]), "sepvad_set_weight_lo")
+        self.weight_lo = mode
 
     def set_split(self, nsplit: int):
         """Concurrent utterance chunks per forward (1..4; bitwise-identical results)."""

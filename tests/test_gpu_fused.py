@@ -20,6 +20,11 @@ SEP_TOL = 1e-4
 VAD_PROB_TOL = 1e-3  # VAD probabilities; labels bit-exact (see test_gpu_parity.VAD_PROB_TOL)
 SCHED_TOL = 1e-5
 VAD_SCHED_TOL = 1e-4
+# the fused TCN's opt-in e4m3 weight lo plane (include/sepvad.h SEPVAD_WLO_E4M3) vs its default fp16 lo plane:
+# different weights below 2^-16 relative, so the two fp32-equivalent results differ by up to about the fp32
+# reference's own distance from fp64 (2.7e-5 on the waveforms), not by summation order alone; VAD
+# probabilities within the VAD head's own sensitivity (VAD_PROB_TOL)
+LO8_TOL = 4e-5
 DEV = "cuda"
 
 
@@ -36,14 +41,32 @@ def nets(state_dicts):
     return out
 
 
-def _run(net, x, fused, ikw=None):
+def _run(net, x, fused, ikw=None, wlo="f16"):
+    net.native_weight_lo = wlo
     h = net.native_handle(DEV)
     h.set_fused(fused)
-    with torch.no_grad():
-        sep, vad, est = net(x, ikw) if ikw is not None else net(x)
-    used = h.fused_status()  # synchronises; raises if a hand-off wait gave up
-    h.set_fused(True)
+    try:
+        with torch.no_grad():
+            sep, vad, est = net(x, ikw) if ikw is not None else net(x)
+        used = h.fused_status()  # synchronises; raises if a hand-off wait gave up
+    finally:
+        h.set_fused(True)
+        net.native_weight_lo = "f16"
     return sep, vad, est, used
+
+
+def _check_schedules(net, x, sf, vf):
+    """Fused (sf, vf: the default fp16 weight lo plane) vs the multi-kernel schedule, and vs the fused kernel with the
+    opt-in e4m3 lo plane."""
+    sm, vm, em, used_m = _run(net, x, False)
+    assert not used_m
+    assert (sf - sm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    s8, v8, _, used = _run(net, x, True, wlo="e4m3")
+    assert used
+    assert (s8 - sf).abs().max().item() <= LO8_TOL
+    assert (v8 - vf).abs().max().item() <= VAD_PROB_TOL
+    return sm, vm, em
 
 
 @pytest.mark.parametrize("cname", CONFIGS)
@@ -73,10 +96,7 @@ def test_fused_vs_multikernel_and_oracle(cname, N, nets, state_dicts):
     net = nets[cname]
     sf, vf, ef, used = _run(net, x.to(DEV), True)
     assert used
-    sm, vm, em, used_m = _run(net, x.to(DEV), False)
-    assert not used_m
-    assert (sf - sm).abs().max().item() <= SCHED_TOL
-    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    sm, vm, em = _check_schedules(net, x.to(DEV), sf, vf)
     assert (ef - em).abs().max().item() <= 1e-3
     om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
     s_ref, v_ref, _ = om(x[:1])
@@ -99,8 +119,7 @@ def test_persistent_groups_cover_large_batches(nets):
     sub = [0, 63, 64, 127, 128, 149]
     c, vc, _, _ = _run(net, x[sub], True)
     assert torch.equal(a[sub], c) and torch.equal(va[sub], vc)
-    m, vm, _, _ = _run(net, x[sub], False)
-    assert (c - m).abs().max().item() <= SCHED_TOL
+    _check_schedules(net, x[sub], c, vc)
 
 
 def test_inference_kw_on_fused(nets):
@@ -114,10 +133,31 @@ def test_inference_kw_on_fused(nets):
 
 
 def test_long_utterances_fall_back(nets):
-    """T > 1024 (N >= 262144) does not fit one group: the multi-kernel schedule runs."""
-    x = torch.rand(1, 262144, device=DEV) * 1.8 - 0.9
+    """T > 4096 (N >= 1048576, 65.5 s) does not fit one group of 128: the multi-kernel schedule runs."""
+    x = torch.rand(1, 1048576, device=DEV) * 1.8 - 0.9
     _, _, _, used = _run(nets["with_vad"], x, True)
     assert not used
+
+
+@pytest.mark.parametrize("N", [262144, 480000, 960000])
+def test_whole_file_forwards_stay_fused(N, nets, state_dicts):
+    """only_inference.py:90-91 forwards a whole file (model/model.py:402-461 has no length limit): 16.4 s, 30 s and 60 s
+    at 16 kHz are G = 33, 59 and 118 workgroups per utterance -- groups that span XCDs (write-through hand-offs), GN2
+    words polled in the first P3 pass's spare slots, moment words in 512-word passes. Fused vs the multi-kernel schedule
+    and vs the oracle on utterance 0."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    x = torch.from_numpy(synth.make_batch(2, N, 5150 + N % 997)[0])
+    sf, vf, _, used = _run(net, x.to(DEV), True)
+    assert used, "the fused TCN did not run"
+    _check_schedules(net, x.to(DEV), sf, vf)
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    s_ref, v_ref, _ = om(x[:1])
+    assert np.abs(sf[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((vf[:1].cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
 
 
 def test_fp32_gemms_use_multikernel(nets):
@@ -181,10 +221,7 @@ def test_long_files_full_chip_groups(nets, state_dicts):
     x = torch.from_numpy(synth.make_batch(8, 256000, 8080)[0])
     sf, vf, _, used = _run(net, x.to(DEV), True)
     assert used
-    sm, vm, _, used_m = _run(net, x.to(DEV), False)
-    assert not used_m
-    assert (sf - sm).abs().max().item() <= SCHED_TOL
-    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    _check_schedules(net, x.to(DEV), sf, vf)
     om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
     s_ref, v_ref, _ = om(x[:1])
     assert np.abs(sf[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL

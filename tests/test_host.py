@@ -99,3 +99,33 @@ def test_resample_filter_matches_restatement():
         k, width, oo, nn = sinc_kernel(o, n)
         assert info == (nn, 2 * width + oo, oo, width)
         assert np.abs(taps - k[:, 0, :].numpy()).max() <= 1e-7
+
+
+def test_e4m3_encoder_matches_torch():
+    """The packer's e4m3 encoder (weight lo plane of the fused TCN, include/sepvad.h SEPVAD_WLO_E4M3) vs torch's
+    float8_e4m3fn cast (OCP, round to nearest even): every finite magnitude class, ties, subnormals, saturation."""
+    import numpy as np
+    import torch
+    from sep_tfanet_vad_amd import native
+    lib = native.load_library()
+    rng = np.random.default_rng(7)
+    x = np.concatenate([
+        rng.standard_normal(20000) * np.exp2(rng.uniform(-12, 9, 20000)),      # every binade of the range
+        # all 256 codes' values and the midpoints between neighbouring codes (ties to even)
+        torch.arange(256, dtype=torch.uint8).view(torch.float8_e4m3fn).float().numpy(),
+        np.array([0.0, -0.0, 2.0 ** -10, 3 * 2.0 ** -11, 2.0 ** -9 * 1.5, 440.0, 448.0, 449.0, 1e4, -1e4]),
+    ]).astype(np.float32)
+    codes = torch.arange(256, dtype=torch.uint8).view(torch.float8_e4m3fn).float().numpy()
+    fin = np.sort(np.unique(codes[np.isfinite(codes)]))
+    x = np.concatenate([x, ((fin[1:] + fin[:-1]) / 2).astype(np.float32)])
+    x = x[np.isfinite(x)]
+    out = np.zeros(x.size, np.uint8)
+    assert lib.sepvad_e4m3_encode(x.ctypes.data, out.ctypes.data, x.size) == 0
+    got = torch.from_numpy(out).view(torch.float8_e4m3fn).float().numpy()
+    want = torch.from_numpy(np.clip(x, -448, 448)).to(torch.float8_e4m3fn).float().numpy()
+    assert np.array_equal(got, want)
+    # the lo plane's range: |lo| <= 2^-12 of a row-scaled weight, stored * 2^19 -> <= 128, 4 significant bits
+    lo = (rng.uniform(-1, 1, 4096) * 2.0 ** -12).astype(np.float32)
+    assert lib.sepvad_e4m3_encode((lo * 2 ** 19).ctypes.data, out.ctypes.data, 4096) == 0
+    back = torch.from_numpy(out[:4096].copy()).view(torch.float8_e4m3fn).float().numpy() / 2 ** 19
+    assert np.all(np.abs(back - lo) <= np.abs(lo) * 2.0 ** -4 + 2.0 ** -29)
