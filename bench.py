@@ -62,11 +62,18 @@ def tcn_flops(B, T, precision="f16x3", nblk=24):
     return nblk * 2 * (256 * 256 + 512 * 256) * B * T
 
 
-def tcn_bytes(B, T, precision="f16x3"):
+def weight_bytes(precision, wlo="f16"):
+    """Bytes per pointwise weight streamed by the fused TCN: fp16 hi + fp16 lo (f16x3), fp16 hi + a byte lo plane
+    (f16x3 with --wlo e4m3 / i8), or one 16-bit plane (f16 / bf16)."""
+    return (4 if wlo == "f16" else 3) if precision == "f16x3" else 2
+
+
+def tcn_bytes(B, T, precision="f16x3", wlo="f16"):
     """Compulsory HBM bytes of one fused-TCN launch: TCN input read + output written (fp32 [B][Tp][256]),
-    the weights in fragment order read once (24 blocks x 768 KB as fp16 hi/lo, 384 KB as one 16-bit plane)."""
+    the weights in fragment order read once (24 blocks x 768 KB as fp16 hi/lo, 576 KB with a byte lo plane,
+    384 KB as one 16-bit plane)."""
     Tp = (T + 63) // 64 * 64
-    wbytes = 4 if precision == "f16x3" else 2
+    wbytes = weight_bytes(precision, wlo)
     return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * wbytes
 
 
@@ -75,13 +82,13 @@ RING_FILE = "r02bi_ring_gemm.txt"       # GEMM-phase stream floor per CU (tools/
 STREAM_FLOOR_GBPS = 103.2
 
 
-def weight_stream(B, T, precision, avg_launch_s, n_cu=256):
+def weight_stream(B, T, precision, avg_launch_s, n_cu=256, wlo="f16"):
     """The fused TCN's per-CU weight stream: every workgroup pulls every block's weights once per 32-frame
     slice it owns, so each CU moves slices x 24 x (256x256 + 512x256) x 4 (fp16 hi/lo) or 2
     bytes per launch. With the texture-path busy fraction from the committed counters where they apply."""
     G = (T + 31) // 32
     slices = -(-B * G // n_cu)
-    wbytes = 4 if precision == "f16x3" else 2
+    wbytes = weight_bytes(precision, wlo)
     per_cu = slices * 24 * (256 * 256 + 256 * 512) * wbytes
     rate = per_cu / avg_launch_s / 1e9
     out = {"bytes_per_cu_per_launch": per_cu, "slices_per_cu": slices, "achieved_GBps_per_cu": round(rate, 2),
@@ -89,7 +96,7 @@ def weight_stream(B, T, precision, avg_launch_s, n_cu=256):
            "floor_GBps_per_cu": STREAM_FLOOR_GBPS, "frac_of_floor": round(rate / STREAM_FLOOR_GBPS, 3),
            "floor_source": "profiles/" + RING_FILE, "ta_busy_frac": None, "ta_source": None}
     path = os.path.join(REPO, "profiles", TA_FILE)
-    if precision == "f16x3" and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
+    if precision == "f16x3" and wlo == "f16" and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
         try:
             lines = open(path).read().splitlines()
             i = next(k for k, ln in enumerate(lines) if "k_tcn" in ln)
@@ -109,7 +116,8 @@ def res_out_bytes(B, T):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r02aw_pmc_tcn.json"      # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r03a_pmc_tcn.json"       # fused schedule (k_tcn)
+PMC_WLO = "f16"                            # ... measured with this weight lo plane
 DEFAULT_SPLIT = 1
 
 
@@ -320,6 +328,9 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32", "bf16", "f16"],
                     help="GEMM arithmetic: f16x3 / fp32 meet the fp32 parity gates (default f16x3); bf16 / f16 are "
                          "the reduced-precision arms (BASELINE cfg 2 / cfg 5; tolerance in DESIGN.md §4)")
+    ap.add_argument("--wlo", default="i8", choices=["f16", "e4m3", "i8"],
+                    help="storage of the f16x3 weight lo plane in the fused TCN (include/sepvad.h SEPVAD_WLO_*): i8 "
+                         "(default) / e4m3 (3 B per weight) or f16 (4 B)")
     ap.add_argument("--workload", default="offline", choices=["offline", "cfg4", "cfg5", "long", "stream"],
                     help="offline: cfg 2 (default, the BASELINE metric: B=64, N=32000); cfg4: 8 s reverberant "
                          "mixtures, B=64/GPU, N=64000 (T=251); cfg5: B=128/GPU, N=32000 (run with --precision "
@@ -350,6 +361,7 @@ def main():
     net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     net = net.eval().to(dev)
     net.native_precision = args.precision
+    net.native_weight_lo = args.wlo
     B0, N0 = {"offline": (B_PER_GPU, N_SAMPLES), "cfg4": (64, 64000), "cfg5": (128, 32000),
               "long": (8, 256000)}[args.workload]
     B = args.batch or B0
@@ -390,7 +402,7 @@ def main():
         res_avg_s = res_ms / n_res / 1e3
         if fused:
             # dominant kernel = the fused persistent TCN (all 24 blocks in one launch)
-            flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision)
+            flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision, args.wlo)
             body = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
                     "512->256, TF-attention, recursive LN], ")
             if args.precision == "f16x3":
@@ -418,7 +430,8 @@ def main():
         # (tools/gpu_round.sh -> tools/pmc.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
         traffic = traffic_src = None
         pmc = os.path.join(REPO, "profiles", pmc_name)
-        if os.path.exists(pmc) and args.precision == "f16x3" and B == B_PER_GPU and N == N_SAMPLES:
+        if (os.path.exists(pmc) and args.precision == "f16x3" and (not fused or args.wlo == PMC_WLO) and B == B_PER_GPU
+                and N == N_SAMPLES):
             try:
                 traffic = round(json.load(open(pmc))["hbm_bytes_per_launch"])
                 traffic_src = "profiles/" + pmc_name
@@ -437,7 +450,7 @@ def main():
             "vs_baseline": None,
             # arithmetic type of the path: fp32 (fp16x3 is an fp32-equivalent split), or the reduced arm's operand
             "dtype": {"f16x3": "fp32", "fp32": "fp32", "bf16": "bf16", "f16": "f16"}[args.precision],
-            "gemm_arithmetic": args.precision,
+            "gemm_arithmetic": args.precision + (f" (weight lo plane {args.wlo})" if args.precision == "f16x3" else ""),
             "split": args.split,
             "schedule": "fused" if fused else "multi-kernel",
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
@@ -473,7 +486,7 @@ def main():
             },
         }
         if fused:
-            out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s)
+            out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s, wlo=args.wlo)
         if world == 1 and not args.no_cpu_baseline and args.workload == "offline":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         emit(out)

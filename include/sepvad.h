@@ -46,14 +46,18 @@ enum { SEPVAD_LN_PLAIN = 0, SEPVAD_LN_RECURSIVE = 1, SEPVAD_LN_RESIDUAL = 2 };
  * rounded to fp16 / bf16, one v_mfma_f32_32x32x16_{f16,bf16} product, fp32 accumulation; everything outside
  * the GEMMs stays fp32. Their tolerance vs fp32 is measured, not gated. */
 enum { SEPVAD_PREC_FP32 = 0, SEPVAD_PREC_F16X3 = 1, SEPVAD_PREC_F16 = 2, SEPVAD_PREC_BF16 = 3 };
-/* Storage of the weight lo plane of F16X3 in the fused TCN (the 1x1 convs of model/model.py:104,114):
- *   F16 (default): w*2^-e = hi + lo, both fp16 (4 bytes per weight streamed);
- *   E4M3: lo stored as OCP e4m3 (scaled by 2^19) and widened to fp16 in registers: 3 bytes per weight. Measured on
- *          MI355X: k_tcn -2.1 % shader cycles at cfg 2; waveforms 3.1e-6 from the oracle (fp16 lo: 3.0e-6), but the
- *          masks / est move by up to 1.4e-5 of their range (fp16 lo: below 1e-5), so it is an opt-in arm.
- *          tools/lo_plane_precision.py emulates it on the CPU.
- * The multi-kernel schedule and the head always use F16. Environment override at create time: SEPVAD_WLO=e4m3. */
-enum { SEPVAD_WLO_E4M3 = 0, SEPVAD_WLO_F16 = 1 };
+/* Storage of the weight lo plane of F16X3 in the fused TCN (the 1x1 convs of model/model.py:104,114); the row-scaled
+ * weight w*2^-e = hi + lo with hi fp16 and |lo| <= 2^-12:
+ *   I8 (default): lo as int8 steps of 2^-19 (biased by 128), widened exactly to fp16 in registers by v_perm_b32 + one
+ *          packed fp16 fma: 3 bytes per weight streamed instead of 4, absolute lo error <= 2^-20 of the row's largest
+ *          weight. k_tcn -1.8 % shader cycles at cfg 2; every parity gate at its fp16-lo bound.
+ *   F16:   lo as fp16 (rounds 1-2; 4 bytes per weight).
+ *   E4M3:  lo as OCP e4m3 (scaled by 2^19), widened by v_cvt_scalef32_pk_f16_fp8: 3 bytes per weight, the cheapest
+ *          widening (k_tcn -4.0 %), but 4 significant bits of lo move masks / est by up to 1.4e-5 of their range
+ *          (others: below 1e-5), so it is opt-in. tools/lo_plane_precision.py emulates the formats on the CPU.
+ * Waveforms stay within 3.1e-6 of the oracle with 0 VAD label flips in all three (tests/test_gpu_precision.py).
+ * The multi-kernel schedule and the head always use F16. Environment override at create time: SEPVAD_WLO=f16|e4m3|i8. */
+enum { SEPVAD_WLO_E4M3 = 0, SEPVAD_WLO_F16 = 1, SEPVAD_WLO_I8 = 2 };
 
 /* SeparationModel kwargs that change the computation (model/model.py:362-366). */
 typedef struct SepVadConfig {
@@ -108,7 +112,7 @@ int32_t sepvad_reserve(sepvad_handle h, int32_t B, int32_t N);
 /* Switch the GEMM arithmetic of later forwards (SEPVAD_PREC_*); weights for both are resident. */
 int32_t sepvad_set_precision(sepvad_handle h, int32_t precision);
 
-/* Weight lo-plane format of the fused TCN for later F16X3 forwards (SEPVAD_WLO_*); both are resident. */
+/* Weight lo-plane format of the fused TCN for later F16X3 forwards (SEPVAD_WLO_*); all three are resident. */
 int32_t sepvad_set_weight_lo(sepvad_handle h, int32_t mode);
 
 /* HOST function: the packer's float -> OCP e4m3fn encoder (round to nearest even, saturating at 448), as used

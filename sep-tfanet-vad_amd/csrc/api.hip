@@ -50,6 +50,7 @@ struct PackedW {
   size_t fhi = 0, flo = 0;  // fused-TCN copies in MFMA B-fragment order (see pack_pointwise)
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
   size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
+  size_t fi8 = 0;           // ... the same as int8 steps of 2^-WQ_LO_SHIFT, biased by 128
 };
 
 struct BlockOff {
@@ -151,9 +152,9 @@ struct sepvad_model {
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU), max over precisions
   int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
   __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered fp16 hi/lo weights (F16X3, SEPVAD_WLO_F16)
-  __half* twq = nullptr;        // [nblk][WQ_BLOCK] fragment-ordered fp16 hi + e4m3 lo weights (F16X3, SEPVAD_WLO_E4M3)
-  int lo8 = 0;                  // k_tcn's weight lo plane: fp16 (0, default) or e4m3 (1); SEPVAD_WLO / sepvad_set_weight_lo
-  int tcn_cap_q = 0;            // co-resident capacity of the e4m3-lo k_tcn
+  __half* twq[3] = {};          // [nblk][WQ_BLOCK] fragment-ordered fp16 hi + byte lo weights: [1] e4m3, [2] int8
+  int lo8 = 2;                  // k_tcn's weight lo plane: 0 fp16, 1 e4m3, 2 int8 (default); SEPVAD_WLO / sepvad_set_weight_lo
+  int tcn_cap_q[3] = {};        // co-resident capacity of the byte-lo k_tcn variants
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
@@ -316,7 +317,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
     p.fbf = pk.addh(fb);
     // e4m3 lo plane: lane l, K-step pair pr -> 16 bytes: j = 0..7 of step 2 pr, then of step 2 pr + 1
     if ((cin / 16) % 2 == 0) {
-      std::vector<uint8_t> f8((size_t)mpad * cin);
+      std::vector<uint8_t> f8((size_t)mpad * cin), i8((size_t)mpad * cin);
       size_t b = 0;
       for (int mt = 0; mt < mpad / 32; ++mt)
         for (int pr = 0; pr < cin / 32; ++pr)
@@ -325,10 +326,15 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
               for (int j = 0; j < 8; ++j, ++b) {
                 const size_t src = (size_t)(32 * mt + (l & 31)) * cin + 16 * (2 * pr + h) + 8 * (l >> 5) + j;
                 f8[b] = e4m3_rn(lo32[src] * (float)(1 << WQ_LO_SHIFT));  // exact power-of-two scaling
+                // int8: |lo| <= 2^-12 -> |q| <= 128; +128 (a tie at half an ulp of hi) saturates to 127
+                const double q = std::nearbyint(std::ldexp((double)lo32[src], WQ_LO_SHIFT));
+                i8[b] = (uint8_t)(std::max(-128.0, std::min(127.0, q)) + 128.0);
               }
       std::vector<__half> f8h(f8.size() / 2);
       std::memcpy(f8h.data(), f8.data(), f8.size());
       p.fl8 = pk.addh(f8h);
+      std::memcpy(f8h.data(), i8.data(), i8.size());
+      p.fi8 = pk.addh(f8h);
     }
   }
   return p;
@@ -462,10 +468,12 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, false);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
   }
-  h->tcn_cap_q = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, true);
-  h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q);
+  for (int q = 1; q <= 2; ++q) {
+    h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q);
+    h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q[q]);
+  }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
-  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk);
+  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
   for (int i = 0; i < h->nblk; ++i) {
@@ -480,6 +488,11 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     std::copy_n(pk.hblob.begin() + bo.w1.fl8, WQ_W2H - WQ_W1L, wqb + WQ_W1L);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WQ_W2L - WQ_W2H, wqb + WQ_W2H);
     std::copy_n(pk.hblob.begin() + bo.w2.fl8, WQ_BLOCK - WQ_W2L, wqb + WQ_W2L);
+    __half* wib = wi.data() + WQ_BLOCK * i;
+    std::copy_n(pk.hblob.begin() + bo.w1.fhi, WQ_W1L, wib);
+    std::copy_n(pk.hblob.begin() + bo.w1.fi8, WQ_W2H - WQ_W1L, wib + WQ_W1L);
+    std::copy_n(pk.hblob.begin() + bo.w2.fhi, WQ_W2L - WQ_W2H, wib + WQ_W2H);
+    std::copy_n(pk.hblob.begin() + bo.w2.fi8, WQ_BLOCK - WQ_W2L, wib + WQ_W2L);
     std::copy_n(pk.hblob.begin() + bo.w1.fhi, WS_W2, ws16.data() + WS_BLOCK * i);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WS_BLOCK - WS_W2, ws16.data() + WS_BLOCK * i + WS_W2);
     std::copy_n(pk.hblob.begin() + bo.w1.fbf, WS_W2, wsbf.data() + WS_BLOCK * i);
@@ -508,8 +521,10 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   }
   HIPCHK(hipMalloc(&h->twf, wf.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&h->twq, wq.size() * sizeof(__half)));
-  HIPCHK(hipMemcpy(h->twq, wq.data(), wq.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twq[1], wq.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twq[1], wq.data(), wq.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twq[2], wi.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twq[2], wi.data(), wi.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twf16, ws16.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf16, ws16.data(), ws16.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twbf, wsbf.size() * sizeof(__half)));
@@ -855,7 +870,8 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     return nullptr;
   }
   if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
-  if (const char* wl = getenv("SEPVAD_WLO")) h->lo8 = std::strcmp(wl, "e4m3") == 0;  // "f16" (default) | "e4m3"
+  if (const char* wl = getenv("SEPVAD_WLO"))  // "i8" (default) | "f16" | "e4m3"
+    h->lo8 = std::strcmp(wl, "e4m3") == 0 ? 1 : (std::strcmp(wl, "f16") == 0 ? 0 : 2);
   if (init_fused(h, pk) != SEPVAD_OK) {
     sepvad_destroy(h);
     return nullptr;
@@ -884,8 +900,9 @@ int32_t sepvad_set_precision(sepvad_handle h, int32_t precision) {
 
 int32_t sepvad_set_weight_lo(sepvad_handle h, int32_t mode) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
-  if (mode != SEPVAD_WLO_E4M3 && mode != SEPVAD_WLO_F16) return fail(SEPVAD_E_ARG, "unknown weight lo-plane format");
-  h->lo8 = mode == SEPVAD_WLO_E4M3;
+  if (mode != SEPVAD_WLO_E4M3 && mode != SEPVAD_WLO_F16 && mode != SEPVAD_WLO_I8)
+    return fail(SEPVAD_E_ARG, "unknown weight lo-plane format");
+  h->lo8 = mode == SEPVAD_WLO_E4M3 ? 1 : (mode == SEPVAD_WLO_I8 ? 2 : 0);
   return SEPVAD_OK;
 }
 
@@ -920,7 +937,7 @@ static_assert(SEPVAD_PREC_FP32 == PREC_F32 && SEPVAD_PREC_F16X3 == PREC_F16X3 &&
 
 // co-resident k_tcn workgroups of the variant that will run (the e4m3-lo kernel is its own instantiation)
 int tcn_cap_of(const sepvad_model* h) {
-  return h->prec == PREC_F16X3 && h->lo8 ? h->tcn_cap_q : h->tcn_cap_p[h->prec];
+  return h->prec == PREC_F16X3 && h->lo8 ? h->tcn_cap_q[h->lo8] : h->tcn_cap_p[h->prec];
 }
 
 bool fused_ok(const sepvad_model* h, int T) {
@@ -1047,8 +1064,8 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
     ta.prec = h->prec;
-    ta.lo8 = h->prec == PREC_F16X3 && h->lo8;
-    ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
+    ta.lo8 = h->prec == PREC_F16X3 ? h->lo8 : 0;
+    ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq[ta.lo8] : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
     ta.prm = h->tprm;
     ta.inv_ch = 1.0 / ((double)CH * T);
     ta.inv_hid = 1.0 / ((double)HID * T);
@@ -1735,7 +1752,8 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->fork) (void)hipEventDestroy(h->fork);
   for (auto& c : h->ctx) free_ctx(c.release());
   if (h->twf) (void)hipFree(h->twf);
-  if (h->twq) (void)hipFree(h->twq);
+  for (__half* q : h->twq)
+    if (q) (void)hipFree(q);
   if (h->twf16) (void)hipFree(h->twf16);
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);

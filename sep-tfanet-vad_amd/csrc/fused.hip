@@ -94,6 +94,9 @@ constexpr int PD = TCN_PD;        // weight K steps in flight per wave
 #ifndef TCN_AD
 #define TCN_AD 1     // GEMM A-fragment LDS reads issued this many K steps ahead (2: no gain, profiles/r03h_ab_*)
 #endif
+#ifndef TCN_XPK
+#define TCN_XPK 1    // x' update: lane pairs pack two channels per 32-bit LDS store (1) or 16-bit stores (0)
+#endif
 #ifndef TCN_PDQ
 #define TCN_PDQ 8    // ... with the e4m3 lo plane (16 fits the registers, 238 VGPRs, but measured 4 % more cycles)
 #endif
@@ -129,8 +132,9 @@ constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
 static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
-template <int PRE, bool L8 = false>
+template <int PRE, int LQ = 0>
 struct WLay {
+  static constexpr bool L8 = LQ != 0;
   static constexpr bool X3 = PRE == PREC_F16X3;
   static constexpr size_t BLOCK = X3 ? (L8 ? WQ_BLOCK : WF_BLOCK) : WS_BLOCK;
   static constexpr size_t W1H = 0, W1L = X3 ? (L8 ? WQ_W1L : WF_W1L) : 0;
@@ -146,22 +150,40 @@ struct WLay {
 // L8 (F16X3 only): the lo plane is e4m3 (sepvad_internal.h WQ_*), one 1 KB wave load per two K steps at
 // voffl + 1024 * pair into rl[i / 2], widened to fp16 in registers (v_cvt_scalef32_pk_f16_fp8, 4 per step,
 // scale 2^-WQ_LO_SHIFT) right before the step's MFMAs: 3 bytes per weight instead of 4.
+// LQ = 2: the lo bytes are int8 steps of 2^-WQ_LO_SHIFT (stored biased, q + 128): v_perm_b32 builds the fp16 values
+// 1024 + byte (0x64XX), and one packed fma scales and unbiases them -- exact (every result is a multiple of 2^-19).
+template <int LQ>
 __device__ __forceinline__ f16x8 lo8_widen(u32x4v q, int half) {
   constexpr float sc = 1.0f / (float)(1 << WQ_LO_SHIFT);
   const unsigned d0 = half ? q[2] : q[0], d1 = half ? q[3] : q[1];
-  const h16x2 c0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, false);
-  const h16x2 c1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, true);
-  const h16x2 c2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, false);
-  const h16x2 c3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, true);
-  return f16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
+  if constexpr (LQ == 1) {
+    const h16x2 c0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, false);
+    const h16x2 c1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, true);
+    const h16x2 c2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, false);
+    const h16x2 c3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, true);
+    return f16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
+  } else {
+    // v_perm_b32(src0, src1, sel): selector byte k picks byte sel_k of {src0:src1} (0..3 = src1, 4..7 = src0)
+    constexpr unsigned M = 0x64646464u;
+    const h16x2 s2 = {(_Float16)sc, (_Float16)sc}, o2 = {(_Float16)(-1152.0f * sc), (_Float16)(-1152.0f * sc)};
+    h16x2 c[4];
+    c[0] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07010700u));  // bytes 0, 1 -> 0x64b0, 0x64b1
+    c[1] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07030702u));  // bytes 2, 3
+    c[2] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07010700u));
+    c[3] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07030702u));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = __builtin_elementwise_fma(c[k], s2, o2);
+    return f16x8{c[0][0], c[0][1], c[1][0], c[1][1], c[2][0], c[2][1], c[3][0], c[3][1]};
+  }
 }
 
-template <int NS, int LDA, int PRE, int RD = PD, bool L8 = false>
+template <int NS, int LDA, int PRE, int RD = PD, int LQ = 0>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
   static_assert(NS % RD == 0 && NS >= RD, "K steps");
-  static_assert(!L8 || (PRE == PREC_F16X3 && RD % 2 == 0), "e4m3 lo plane: F16X3, K-step pairs");
+  constexpr bool L8 = LQ != 0;
+  static_assert(!L8 || (PRE == PREC_F16X3 && RD % 2 == 0), "byte lo plane: F16X3, K-step pairs");
   constexpr bool X3 = PRE == PREC_F16X3;
   const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
   // A fragments AD steps ahead: the LDS reads of step s+AD are in flight during steps s..s+AD-1 (AD = 2: a wave that
@@ -200,7 +222,7 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
     } else if constexpr (X3) {
       const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
       f16x8 bl;
-      if constexpr (L8) bl = lo8_widen(rl[i >> 1], i & 1);
+      if constexpr (L8) bl = lo8_widen<LQ>(rl[i >> 1], i & 1);
       else bl = __builtin_bit_cast(f16x8, rl[i]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
@@ -240,9 +262,10 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
 }
 
-template <int PRE, int RD = PD, bool L8 = false>
+template <int PRE, int RD = PD, int LQ = 0>
 __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                            u32x4v (&rh)[RD], u32x4v (&rl)[RD]) {
+  constexpr bool L8 = LQ != 0;
 #pragma unroll
   for (int s = 0; s < RD; ++s) {
     rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
@@ -256,9 +279,10 @@ __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_b
 
 // Ring entry s only (the burst above spread over a phase's rows: a CU's texture path takes one 1 KB wave load
 // per ~16 clocks, so 8 waves issuing the whole ring at once stall ~1 us on issue)
-template <int PRE, int RD, bool L8 = false>
+template <int PRE, int RD, int LQ = 0>
 __device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                             u32x4v (&rh)[RD], u32x4v (&rl)[RD], int s) {
+  constexpr bool L8 = LQ != 0;
   rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
   if constexpr (L8) {
     if (s % 2 == 0) rl[s / 2] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, (s / 2) * 1024, 0);
@@ -340,9 +364,10 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   }
 }
 
-template <int LM, int PRE, bool DUMP = false, bool L8 = false>
+template <int LM, int PRE, bool DUMP = false, int LQ = 0>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
-  using WL = WLay<PRE, L8>;
+  using WL = WLay<PRE, LQ>;
+  constexpr bool L8 = LQ != 0;
   constexpr int RD = L8 ? TCN_PDQ : PD;  // weight K steps in flight per wave
   constexpr int RPI = RD / 8;            // ring entries issued per row of the phases before the GEMMs (8 row steps)
   static_assert(RD % 8 == 0 && RD <= 16, "ring depth: 8 or 16 K steps");
@@ -424,7 +449,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       pb[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, co, 0, 0));
       pg[1] = pb[1] = 0.f;
       sx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc_of(ka->prm), 0, PB_SX * 4, 0));
-      prefetch_w<PRE, RD, L8>(w1h, w1l, voffu, voffu_l, rh, rl);  // block-0 conv1d weights: in flight with the input rows
+      prefetch_w<PRE, RD, LQ>(w1h, w1l, voffu, voffu_l, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
     if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
@@ -511,7 +536,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS1, LDX, PRE, RD, L8>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, voff1l, rh, rl, lane);
+        wave_gemm<NS1, LDX, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, voff1l, rh, rl, lane);
       TPROBE(1);
       }
       {
@@ -615,7 +640,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #endif
         // res_out weights: in flight during the depthwise conv (issued after the polls: vmcnt retires in
         // order, so no wait above sits behind the weight stream)
-        if (!TCN_PFX) prefetch_w<PRE, RD, L8>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl);
+        if (!TCN_PFX) prefetch_w<PRE, RD, LQ>(rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl);
         __syncthreads();  // halo rows and every member's GN1 words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
@@ -671,7 +696,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           for (int i = 0; i < FR / 4; ++i) {
 #pragma unroll
             for (int e = 0; e < RPI; ++e)  // res_out ring entries RPI i .. RPI i + RPI - 1
-              if (TCN_PFX) prefetch_w1<PRE, RD, L8>(w2h, w2l, voff2, voff2l, rh, rl, RPI * i + e);
+              if (TCN_PFX) prefetch_w1<PRE, RD, LQ>(w2h, w2l, voff2, voff2l, rh, rl, RPI * i + e);
             const int tl = fr0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;
             f32x2 y[2];
@@ -714,7 +739,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int i = 0; i < FR / 2; ++i) {
             // res_out weights: ring entry i/2 in flight from here through the GN2 exchange
-            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE, RD, L8>(w2h, w2l, voff2, voff2l, rh, rl, i / 2);
+            if (TCN_PFX && i % 2 == 0) prefetch_w1<PRE, RD, LQ>(w2h, w2l, voff2, voff2l, rh, rl, i / 2);
             const int tl = rh0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;  // mask multiply: no per-output branch
             float dv[2];
@@ -753,7 +778,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       {
-        wave_gemm<NS2, LDD, PRE, RD, L8>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl,
+        wave_gemm<NS2, LDD, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + WL::W2H), rsrc_of(wb + WL::W2L), voff2, voff2l, rh, rl,
                                          lane);
       TPROBE(5);
       }
@@ -1200,7 +1225,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
       const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
       const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
-      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl);
+      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl);
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
@@ -1210,18 +1235,19 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         for (int r = 0; r < 16; r += 2) {
 #pragma unroll
           for (int e = 0; e < RPI; ++e)
-            if (TCN_PFX) prefetch_w1<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl, RPI * (r / 2) + e);
+            if (TCN_PFX) prefetch_w1<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl, RPI * (r / 2) + e);
           const int tl = trow(r);
           const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r], rv[r + 1]}, kc);  // rv gated above
           const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
           const f32x2 ov = x * vm;
           o[r] = ov.x; o[r + 1] = ov.y;
-          split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn);
+          if (TCN_XPK) split_store_rows_pk<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn, (lane & 1) != 0);
+          else split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn);
         }
 #else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE, RD, L8>(wnh, wnl, voff1, voff1l, rh, rl, r / 2);
+          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
@@ -1438,23 +1464,23 @@ hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int PRE, bool L8>
+template <int PRE, int LQ>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
   if constexpr (PRE == PREC_F16X3) {
     if (a.dump != nullptr) {  // parity-probe instantiation (the probe code stays out of the production kernels)
       switch (a.ln_mode) {
-        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
     }
   }
   switch (a.ln_mode) {
-    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, false, L8>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1464,30 +1490,38 @@ hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
   if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || grid < a.G || grid % a.G)
     return hipErrorInvalidValue;
   switch (a.prec) {
-    case PREC_F16X3: return a.lo8 ? launch_tcn_pre<PREC_F16X3, true>(a, grid, s) : launch_tcn_pre<PREC_F16X3, false>(a, grid, s);
-    case PREC_F16: return launch_tcn_pre<PREC_F16, false>(a, grid, s);
-    case PREC_BF16: return launch_tcn_pre<PREC_BF16, false>(a, grid, s);
+    case PREC_F16X3:
+      switch (a.lo8) {
+        case 0: return launch_tcn_pre<PREC_F16X3, 0>(a, grid, s);
+        case 1: return launch_tcn_pre<PREC_F16X3, 1>(a, grid, s);
+        case 2: return launch_tcn_pre<PREC_F16X3, 2>(a, grid, s);
+      }
+      return hipErrorInvalidValue;
+    case PREC_F16: return launch_tcn_pre<PREC_F16, 0>(a, grid, s);
+    case PREC_BF16: return launch_tcn_pre<PREC_BF16, 0>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }
 
-template <int PRE, bool L8>
+template <int PRE, int LQ>
 static int blocks_per_cu_pre(int ln_mode) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
   switch (ln_mode) {
-    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE, PRE, false, L8>, NTHR, 0); break;
-    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE, false, L8>, NTHR, 0); break;
-    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE, false, L8>, NTHR, 0); break;
+    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RECURSIVE, PRE, false, LQ>, NTHR, 0); break;
+    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE, false, LQ>, NTHR, 0); break;
+    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE, false, LQ>, NTHR, 0); break;
   }
   return e == hipSuccess ? nb : 0;
 }
 
-int tcn_blocks_per_cu(int ln_mode, int prec, bool lo8) {
+int tcn_blocks_per_cu(int ln_mode, int prec, int lo) {
   switch (prec) {
-    case PREC_F16X3: return lo8 ? blocks_per_cu_pre<PREC_F16X3, true>(ln_mode) : blocks_per_cu_pre<PREC_F16X3, false>(ln_mode);
-    case PREC_F16: return blocks_per_cu_pre<PREC_F16, false>(ln_mode);
-    case PREC_BF16: return blocks_per_cu_pre<PREC_BF16, false>(ln_mode);
+    case PREC_F16X3:
+      return lo == 1 ? blocks_per_cu_pre<PREC_F16X3, 1>(ln_mode)
+                     : (lo == 2 ? blocks_per_cu_pre<PREC_F16X3, 2>(ln_mode) : blocks_per_cu_pre<PREC_F16X3, 0>(ln_mode));
+    case PREC_F16: return blocks_per_cu_pre<PREC_F16, 0>(ln_mode);
+    case PREC_BF16: return blocks_per_cu_pre<PREC_BF16, 0>(ln_mode);
   }
   return 0;
 }

@@ -310,7 +310,7 @@ constexpr size_t WQ_W1L = 65536, WQ_W2H = 98304, WQ_W2L = 229376, WQ_BLOCK = 294
 constexpr int WQ_LO_SHIFT = 19;
 struct TcnArgs {
   int B, T, Tp, G, nblk, layer, ln_mode, tf_att, prec;
-  int lo8;               // F16X3: the weight lo plane is e4m3 (WQ_* layout) instead of fp16 (WF_*)
+  int lo8;               // F16X3 weight lo plane: 0 fp16 (WF_* layout), 1 e4m3, 2 int8 (WQ_* layout)
   const __half* wfrag;   // [nblk][WF_BLOCK | WQ_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
   const float* prm;      // [nblk][PB_SIZE] parameter blobs
   const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
@@ -355,7 +355,7 @@ struct HeadArgs {
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 hipError_t launch_head(const HeadArgs& a, hipStream_t s);
-int tcn_blocks_per_cu(int ln_mode, int prec, bool lo8);
+int tcn_blocks_per_cu(int ln_mode, int prec, int lo);
 // host: float -> e4m3fn (OCP FP8, bias 7, max 448, no inf), round to nearest even, saturating
 uint8_t e4m3_rn(float x);
 

@@ -192,6 +192,29 @@ __device__ __forceinline__ void split_store_rows(_Float16* hi, _Float16* lo, int
     reinterpret_cast<__bf16*>(hi)[idx] = h.x; reinterpret_cast<__bf16*>(hi)[idx + ld] = h.y;
   }
 }
+// split_store_rows with the lane pair (2c, 2c+1) packing its two channels into 32-bit stores: the even lane writes
+// channels (m, m+1) of frame tl, the odd lane channels (m-1, m) of frame tl+1, each taking the partner's 16-bit value
+// through one DPP swap (quad_perm [1,0,3,2]) and one v_perm: half the LDS store instructions of split_store_rows.
+// idx = the lane's element for frame tl (as split_store_rows); every lane of the wave must take part (DPP).
+template <int PRE>
+__device__ __forceinline__ void split_store_rows_pk(_Float16* hi, _Float16* lo, int idx, int ld, f32x2 v, bool odd) {
+  const unsigned sel = odd ? 0x03020706u : 0x05040100u;  // odd: {partner.y, own.y}; even: {own.x, partner.x}
+  const int at = odd ? idx + ld - 1 : idx;                // 4-byte aligned (m - 1 even / m even)
+  auto put = [&](_Float16* plane, unsigned own) {
+    const unsigned nbr = (unsigned)__builtin_amdgcn_update_dpp(0, (int)own, 0xb1, 0xf, 0xf, false);
+    *reinterpret_cast<unsigned*>(plane + at) = __builtin_amdgcn_perm(nbr, own, sel);
+  };
+  if constexpr (PRE == PREC_F16X3) {
+    const f16x2v h = __builtin_convertvector(v, f16x2v);
+    const f16x2v l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2v);
+    put(hi, __builtin_bit_cast(unsigned, h));
+    put(lo, __builtin_bit_cast(unsigned, l));
+  } else if constexpr (PRE == PREC_F16) {
+    put(hi, __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2v)));
+  } else {
+    put(hi, __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2v)));
+  }
+}
 // resid_apply (device_common.h) on two frames of one channel: kc = {GN_a scale, shift, GN_b scale, shift}
 template <int MODE>
 __device__ __forceinline__ f32x2 resid_apply2(f32x2 o, f32x2 r, const float (&kc)[4]) {

@@ -160,9 +160,9 @@ class SeparationModel(nn.Module):
         # GEMM arithmetic of the native path: "f16x3" (fp32-equivalent split on fp16 MFMA, default)
         # or "fp32" (fp32 MFMA); both meet the fp32 parity gates. SEPVAD_PRECISION overrides.
         self.native_precision = os.environ.get("SEPVAD_PRECISION", "f16x3")
-        # storage of the f16x3 weight lo plane in the fused TCN: "f16" (default) or "e4m3" (opt-in, 3 B per weight
-        # streamed; include/sepvad.h SEPVAD_WLO_*); SEPVAD_WLO overrides
-        self.native_weight_lo = os.environ.get("SEPVAD_WLO", "f16")
+        # storage of the f16x3 weight lo plane in the fused TCN: "i8" (default, 3 B per weight streamed), "f16" or
+        # "e4m3" (include/sepvad.h SEPVAD_WLO_*); SEPVAD_WLO overrides
+        self.native_weight_lo = os.environ.get("SEPVAD_WLO", "i8")
 
     # -- native handle -------------------------------------------------------------------------
     # The handle (folded, packed device weights) is rebuilt lazily after load_state_dict(),

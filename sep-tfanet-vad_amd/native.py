@@ -20,7 +20,7 @@ SEPVAD_PREC_FP32, SEPVAD_PREC_F16X3, SEPVAD_PREC_F16, SEPVAD_PREC_BF16 = 0, 1, 2
 # fp32 / f16x3: fp32-equivalent (parity path); f16 / bf16: reduced-precision arms (tolerance measured)
 PRECISIONS = {"fp32": SEPVAD_PREC_FP32, "f16x3": SEPVAD_PREC_F16X3, "f16": SEPVAD_PREC_F16, "bf16": SEPVAD_PREC_BF16}
 # storage of the f16x3 weight lo plane in the fused TCN (include/sepvad.h SEPVAD_WLO_*)
-WEIGHT_LO = {"e4m3": 0, "f16": 1}
+WEIGHT_LO = {"e4m3": 0, "f16": 1, "i8": 2}
 
 EXPORTED_SYMBOLS = (
     "sepvad_create", "sepvad_reserve", "sepvad_set_precision", "sepvad_set_weight_lo", "sepvad_e4m3_encode",
@@ -238,7 +238,7 @@ class Handle:
         self.precision = precision
 
     def set_weight_lo(self, mode: str):
-        """Weight lo plane of the fused TCN's f16x3 GEMMs: "f16" (default) or "e4m3" (opt-in, 3 B per weight)."""
+        """Weight lo plane of the fused TCN's f16x3 GEMMs: "i8" (default) / "e4m3" (3 B per weight) or "f16"."""
         _check(self._lib.sepvad_set_weight_lo(self._h, WEIGHT_LO[mode]), "sepvad_set_weight_lo")
         self.weight_lo = mode
 

@@ -38,13 +38,13 @@ def _model(cname, state_dicts):
     return net.eval().to(DEV)
 
 
-# f16x3 (fp16 weight lo plane, default), f16x3 with the opt-in e4m3 weight lo plane in the fused TCN, fp32 MFMA
-@pytest.fixture(scope="module", params=["f16x3", "f16x3-e4m3lo", "fp32"])
+# f16x3 (default: int8 weight lo plane in the fused TCN), f16x3 with the fp16 / e4m3 lo planes, fp32 MFMA
+@pytest.fixture(scope="module", params=["f16x3", "f16x3-f16lo", "f16x3-e4m3lo", "fp32"])
 def models(request, state_dicts):
     out = {c: _model(c, state_dicts) for c in CONFIGS}
     for m in out.values():
         m.native_precision = request.param.split("-")[0]
-        m.native_weight_lo = "e4m3" if request.param.endswith("e4m3lo") else "f16"
+        m.native_weight_lo = request.param.split("-")[1][:-2] if "-" in request.param else "i8"
     return out
 
 

@@ -36,6 +36,11 @@ def quant(w, mode):
         sh = int(mode[3:] or 19)  # lo * 2^sh into e4m3 (|lo| <= 2^-12 -> <= 2^(sh-12) <= 448)
         l8 = (lo * 2.0 ** sh).to(torch.float8_e4m3fn).to(torch.float32) / 2.0 ** sh
         q = hi + l8.to(torch.float16).to(torch.float32)   # the MFMA's B_lo operand is fp16
+    elif mode == "lo_i8":
+        # lo as int8 steps of 2^-19 (row-scaled weights: |lo| <= 2^-12 -> |q| <= 128; the packer re-rounds hi when q
+        # would be +128), widened exactly in fp16 by the 1024-magic-number trick
+        q = torch.clamp(torch.round(lo * 2.0 ** 19), -128, 127)
+        q = hi + (q / 2.0 ** 19).to(torch.float16).to(torch.float32)
     elif mode == "lo_bf16":
         q = hi + lo.to(torch.bfloat16).to(torch.float32)
     else:
@@ -63,13 +68,16 @@ def main():
     x, _ = synth.make_batch(B, N, 60_000 + B)
     x = torch.from_numpy(x)
     ref = OracleModel(config_of("with_vad"), sd, torch.float64)(x.to(torch.float64))
-    for mode in ("fp32", "f16x3", "lo8", "lo816", "lo_bf16", "f16"):
-        sep, vad, _ = run(mode, sd, x)
+    modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["fp32", "f16x3", "lo8", "lo_i8", "lo_bf16", "f16"]
+    erange = max(ref[2].real.abs().max().item(), ref[2].imag.abs().max().item())
+    for mode in modes:
+        sep, vad, est = run(mode, sd, x)
         err = (sep.double() - ref[0]).abs().max().item()
         flips = int(((vad >= 0.5) != (ref[1] >= 0.5)).sum())
         verr = (vad.double() - ref[1]).abs().max().item()
-        print(f"{mode:8s} sep max-abs vs fp64 {err:.3e}  vad max-abs {verr:.3e}  label flips {flips}/{vad.numel()}",
-              flush=True)
+        eerr = (est.to(torch.complex128) - ref[2]).abs().max().item() / erange
+        print(f"{mode:8s} sep max-abs vs fp64 {err:.3e}  est {eerr:.2e} of range  vad max-abs {verr:.3e}  "
+              f"label flips {flips}/{vad.numel()}", flush=True)
 
 
 if __name__ == "__main__":
