@@ -189,19 +189,8 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
   // A fragments AD steps ahead: the LDS reads of step s+AD are in flight during steps s..s+AD-1 (AD = 2: a wave that
   // has the SIMD's matrix pipe to itself -- the other wave of the SIMD done with its GEMM -- issues a step every ~96
   // cycles, shorter than an LDS read under load)
-#if TCN_AD == 0  // round-2 form (one step ahead, copies)
-  f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + aoff);
-  f16x8 al = ah;
-  if constexpr (X3) al = *reinterpret_cast<const f16x8*>(Alo + aoff);
-  auto step = [&](int s, int i, bool pf) {
-    f16x8 nh = ah, nl = al;
-    if (s + 1 < NS) {
-      nh = *reinterpret_cast<const f16x8*>(Ahi + aoff + 16 * (s + 1));
-      if constexpr (X3) nl = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + 1));
-    }
-    constexpr int AD = 1;
-#else
   constexpr int AD = TCN_AD;
+  static_assert(AD >= 1, "A-read depth");
   f16x8 aH[AD + 1], aL[AD + 1];
 #pragma unroll
   for (int k = 0; k < AD; ++k) {
@@ -216,7 +205,6 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       if constexpr (X3) aL[nxt] = *reinterpret_cast<const f16x8*>(Alo + aoff + 16 * (s + AD));
     }
     const f16x8 ah = aH[cur], al = aL[cur];
-#endif
     if constexpr (TCN_DIAG == 2) {
       acc[0] += (float)ah[0] + (float)al[0] + __builtin_bit_cast(float, rh[i][0]) + __builtin_bit_cast(float, rl[i][0]);
     } else if constexpr (X3) {
@@ -241,9 +229,6 @@ __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, con
       if constexpr (L8) rl[i >> 1] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, ((s + RD) >> 1) * 1024, 0);
       else rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (s + RD) * 1024, 0);
     }
-#if TCN_AD == 0
-    ah = nh; al = nl;
-#endif
     // pipeline shape of a step: step s+AD's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
     if (s + AD < NS) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 : 1, 0);
