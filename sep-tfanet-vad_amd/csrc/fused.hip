@@ -294,7 +294,7 @@ __device__ __forceinline__ void gn_affine_ch(int tid, const double* acc, int T, 
 // same points (lane 0 of each wave) after that region: probe[grid*nblk*16 + ((blockIdx*nblk + block)*16 + point)*8 + wave]
 #define TPROBE(k)                                                                                  \
   do {                                                                                             \
-    if (a.probe != nullptr && (tid & 63) == 0 && u == grp) {                                       \
+    if (TP_ON && (tid & 63) == 0 && u == grp) {                                                   \
       const unsigned long long _t = wall_clock64();                                                \
       const size_t _i = ((size_t)blockIdx.x * a.nblk + bi) * 16 + (k);                            \
       if (tid == 0) a.probe[_i] = _t;                                                              \
@@ -349,8 +349,10 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   }
 }
 
-template <int LM, int PRE, bool DUMP = false, int LQ = 0>
+template <int LM, int PRE, bool DUMP = false, int LQ = 0, bool PROBE = false>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
+  // phase stamps only in the probe instantiation (SEPVAD_TCN_PROBE): none of their pointers or branches in production
+  const bool TP_ON = PROBE && a.probe != nullptr;
   using WL = WLay<PRE, LQ>;
   constexpr bool L8 = LQ != 0;
   constexpr int RD = L8 ? TCN_PDQ : PD;  // weight K steps in flight per wave
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   unsigned ep = 1;  // epochs published so far (identical sequence in every member); epoch 1 = XCD ids
   // epoch 1: the members' XCD ids (write-through); if the whole group shares one XCD, every later
   // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
-  if (a.probe != nullptr && tid == 0) {  // entry: wall clock, and the shader clock (s_memtime) when nblk > 5
+  if (TP_ON && tid == 0) {  // entry: wall clock, and the shader clock (s_memtime) when nblk > 5
     a.probe[(size_t)blockIdx.x * a.nblk * 16 + 15] = wall_clock64();
     if (a.nblk > 5) a.probe[((size_t)blockIdx.x * a.nblk + 3) * 16 + 15] = __builtin_amdgcn_s_memtime();
   }
@@ -437,9 +439,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       prefetch_w<PRE, RD, LQ>(w1h, w1l, voffu, voffu_l, rh, rl);  // block-0 conv1d weights: in flight with the input rows
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
+    if (TP_ON && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
     reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
-    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 7) * 16 + 15] = wall_clock64();
+    if (TP_ON && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 7) * 16 + 15] = wall_clock64();
     if (u == grp) {
       // the members' XCD ids (write-through, epoch 1); if the whole group shares one XCD, every later
       // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
@@ -453,10 +455,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       bool same = a.xmode == 0;
       for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
       l2 = same;
-      if (a.probe != nullptr && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
+      if (TP_ON && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
     }
     __syncthreads();  // LN record sums (sm.dred) complete
-    if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 2) a.probe[((size_t)blockIdx.x * a.nblk + 2) * 16 + 15] = wall_clock64();
+    if (TP_ON && tid == 0 && u == grp && a.nblk > 2) a.probe[((size_t)blockIdx.x * a.nblk + 2) * 16 + 15] = wall_clock64();
     {  // gn_affine with this iteration's thread id (channel tid < CH)
       float mu, rs;
       gn_moments(sm.dred[0], sm.dred[1], (double)CH * T, a.ln.eps, mu, rs);
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int m = mo_, tid = tido, lane = tid & 63, hl = hl4o >> 2, wave = wave_s;
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
-      if (a.probe != nullptr && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
+      if (TP_ON && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
         a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
       const __half* wb = a.wfrag + (size_t)bi * WL::BLOCK;
       const int li = bi % a.layer;
@@ -1263,10 +1265,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       __syncthreads();
     }
   }
-  if (a.clk != nullptr && threadIdx.x == 0) {
+  // (the clock record pointer re-read from the kernarg segment: nothing held in registers across the blocks)
+  if (unsigned long long* const ck = kargs()->clk; ck != nullptr && threadIdx.x == 0) {
     const unsigned long long rt = wall_clock64();
-    if (blockIdx.x == 0) { a.clk[3] = rt; a.clk[5] = __builtin_amdgcn_s_memtime(); }
-    __hip_atomic_fetch_max(a.clk + 1, rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) { ck[3] = rt; ck[5] = __builtin_amdgcn_s_memtime(); }
+    __hip_atomic_fetch_max(ck + 1, rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1461,6 +1464,10 @@ static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
       }
       return hipGetLastError();
     }
+  }
+  if (a.probe != nullptr && a.ln_mode == LD_RECURSIVE) {  // phase-stamp instantiation (SEPVAD_TCN_PROBE, recursive LN)
+    hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ, true>), dim3(grid), dim3(NTHR), 0, s, a);
+    return hipGetLastError();
   }
   switch (a.ln_mode) {
     case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
