@@ -116,7 +116,7 @@ def res_out_bytes(B, T):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r03o_pmc_tcn.json"       # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r03ab_pmc_tcn.json"       # fused schedule (k_tcn)
 PMC_WLO = "i8"                             # ... measured with this weight lo plane
 DEFAULT_SPLIT = 1
 

@@ -139,12 +139,13 @@ def test_long_utterances_fall_back(nets):
     assert not used
 
 
-@pytest.mark.parametrize("N", [262144, 480000, 960000])
+@pytest.mark.parametrize("N", [262144, 480000, 960000, 1048320])
 def test_whole_file_forwards_stay_fused(N, nets, state_dicts):
-    """only_inference.py:90-91 forwards a whole file (model/model.py:402-461 has no length limit): 16.4 s, 30 s and 60 s
-    at 16 kHz are G = 33, 59 and 118 workgroups per utterance -- groups that span XCDs (write-through hand-offs), GN2
-    words polled in the first P3 pass's spare slots, moment words in 512-word passes. Fused vs the multi-kernel schedule
-    and vs the oracle on utterance 0."""
+    """only_inference.py:90-91 forwards a whole file (model/model.py:402-461 has no length limit): 16.4 s, 30 s, 60 s and
+    65.5 s at 16 kHz are G = 33, 59, 118 and 128 workgroups per utterance -- groups that span XCDs (write-through
+    hand-offs), GN2 words polled in the first P3 pass's spare slots, moment words in 512-word passes; N = 1048320 is
+    T = 4096, the largest fused utterance (N = 1048576, T = 4097, is test_long_utterances_fall_back). Fused vs the
+    multi-kernel schedule and vs the oracle on utterance 0."""
     from oracle.torch_ref import OracleModel
     from sep_tfanet_vad_amd import synth
     net = nets["with_vad"]

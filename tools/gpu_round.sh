@@ -22,6 +22,6 @@ step smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(
        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $out/pmc_fetch.log 2>&1 \
 && step pmc_write && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run \
        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $out/pmc_write.log 2>&1 \
-&& python3 tools/pmc.py $out/pmc_fetch $out/pmc_write "k_tcn<2, 1, false, 2>" $out/pmc_tcn.json \
+&& python3 tools/pmc.py $out/pmc_fetch $out/pmc_write "k_tcn<2, 1, false, 2, false>" $out/pmc_tcn.json \
 && python3 tools/kstats.py $(find $out/prof -name "*kernel_stats.csv" | head -1) \
 && step done
