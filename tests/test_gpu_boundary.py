@@ -249,3 +249,28 @@ def test_profiler_range_around_forward():
         net(x)
     torch.cuda.synchronize()
     assert any(e.name == "sepvad.forward" for e in prof.events())
+
+
+def test_shortest_input_and_too_short_input(net, state_dicts):
+    """torch.stft(center=True, pad_mode="reflect") of the reference (model/model.py:16-25,408) needs N > n_fft / 2 = 256:
+    N = 257 (T = 2) is the shortest forward and matches the oracle; N = 256 raises like the reference's own STFT does
+    (sepvad_forward returns SEPVAD_E_SHAPE -> RuntimeError) instead of returning anything."""
+    from oracle.torch_ref import OracleModel
+    om = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)
+    x = torch.rand(2, 257, generator=torch.Generator().manual_seed(257)) * 1.8 - 0.9
+    with torch.no_grad():
+        s, v, _ = net(x.to(DEV))
+    s_ref, v_ref, _ = om(x)
+    assert s.shape == s_ref.shape and v.shape == v_ref.shape
+    assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    vr = v_ref.numpy()
+    safe = np.abs(vr - 0.5) > 1e-4
+    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    x = x[:, :256].contiguous()
+    with pytest.raises(RuntimeError):
+        om(x)
+    with pytest.raises(RuntimeError), torch.no_grad():
+        net(x.to(DEV))
+    with torch.no_grad():  # the handle stays usable after the refused call
+        s2, _, _ = net(torch.rand(1, 8000, generator=torch.Generator().manual_seed(1)).to(DEV) * 1.8 - 0.9)
+    assert torch.isfinite(s2).all()
