@@ -51,6 +51,10 @@ struct PackedW {
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
   size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
   size_t fi8 = 0;           // ... the same as int8 steps of 2^-WQ_LO_SHIFT, biased by 128
+  // k_tcn16 (fused16.hip, v_mfma_f32_16x16x32) B-fragment order: fp16 planes [mpad/16 tiles][cin/32 steps][64][8 halves],
+  // lane l -> row 16 nt + (l & 15), k = 32 s + 8 (l >> 4) + j; byte planes [mpad/32 tile pairs][cin/32][64][16 bytes:
+  // 8 of tile 2 pp, then 8 of tile 2 pp + 1]
+  size_t ghi = 0, glo = 0, gbf = 0, gf8 = 0, gi8 = 0;
 };
 
 struct BlockOff {
@@ -111,10 +115,13 @@ struct StreamCtx {
   unsigned* herr = nullptr;             // host-mapped copy (pinned, written by the kernel)
   unsigned* herr_dev = nullptr;         // its device address
   unsigned reported = 0;                // last give-up word already returned to the caller
+  unsigned pending = 0;                 // a give-up seen when the salt wrapped (words re-zeroed), not yet reported
   unsigned tsalt = 0;                   // launch counter (hand-off tag salt)
   int last_B = 0, last_N = 0;           // shape of the last forward on this stream (sepvad_side_outputs)
-  long long seq = 0;                    // forwards enqueued on this stream (side outputs are tied to one)
+  long long seq = 0;                    // handle-wide id of the last forward on this stream (side outputs are tied to one)
   unsigned long long used = 0;          // LRU stamp (context cap, get_ctx)
+  hipEvent_t done = nullptr;            // recorded after every enqueue on this context: eviction waits on it (the
+                                        // caller's stream itself may already be destroyed by then)
 };
 
 }  // namespace
@@ -158,6 +165,10 @@ struct sepvad_model {
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
+  // k_tcn16 (fused16.hip: 16-frame members, two workgroups per CU) for T <= 16 * FG16_MAX; opt-in (SEPVAD_TCN16=1)
+  bool tcn16 = false;
+  char* t16w[5] = {};           // [nblk][tcn16_block_bytes] blobs: [0..2] F16X3 with the fp16 / e4m3 / int8 lo plane, [3] F16, [4] BF16
+  int tcn16_cap[5] = {};        // co-resident k_tcn16 workgroups per variant
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
   float* tdump = nullptr;       // parity probe buffer of the fused TCN (sepvad_set_tcn_dump), caller-owned
@@ -165,6 +176,8 @@ struct sepvad_model {
   // enqueue of concurrent callers (the kernels of different streams still overlap on the device)
   std::vector<std::unique_ptr<StreamCtx>> ctx;
   std::mutex mu;
+  unsigned long long use_clock = 0;  // LRU clock of the contexts (under mu)
+  long long fwd_seq = 0;             // forwards enqueued on this handle (under mu): StreamCtx::seq
   int res_B = 0, res_N = 0;     // sepvad_reserve hint: every context's workspace is sized at least this
   unsigned long long* kprobe = nullptr;  // SEPVAD_TAIL_PROBE diagnostics: [workgroups][8]
   unsigned long long* tprobe = nullptr;  // SEPVAD_TCN_PROBE diagnostics: [tcn_cap][nblk][16]
@@ -337,6 +350,36 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
       p.fi8 = pk.addh(f8h);
     }
   }
+  if (mpad % 32 == 0 && cin % 32 == 0) {
+    const size_t n = (size_t)mpad * cin;
+    std::vector<__half> gh(n), gl(n), gb(n);
+    std::vector<uint8_t> g8(n), gi(n);
+    size_t q = 0;
+    for (int nt = 0; nt < mpad / 16; ++nt)
+      for (int st = 0; st < cin / 32; ++st)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j, ++q) {
+            const size_t src = (size_t)(16 * nt + (l & 15)) * cin + 32 * st + 8 * (l >> 4) + j;
+            gh[q] = hi[src]; gl[q] = lo[src]; gb[q] = bf[src];
+          }
+    size_t b = 0;
+    for (int pp = 0; pp < mpad / 32; ++pp)
+      for (int st = 0; st < cin / 32; ++st)
+        for (int l = 0; l < 64; ++l)
+          for (int h = 0; h < 2; ++h)
+            for (int j = 0; j < 8; ++j, ++b) {
+              const size_t src = (size_t)(32 * pp + 16 * h + (l & 15)) * cin + 32 * st + 8 * (l >> 4) + j;
+              g8[b] = e4m3_rn(lo32[src] * (float)(1 << WQ_LO_SHIFT));
+              const double qv = std::nearbyint(std::ldexp((double)lo32[src], WQ_LO_SHIFT));
+              gi[b] = (uint8_t)(std::max(-128.0, std::min(127.0, qv)) + 128.0);
+            }
+    p.ghi = pk.addh(gh); p.glo = pk.addh(gl); p.gbf = pk.addh(gb);
+    std::vector<__half> tmp(n / 2);
+    std::memcpy(tmp.data(), g8.data(), n);
+    p.gf8 = pk.addh(tmp);
+    std::memcpy(tmp.data(), gi.data(), n);
+    p.gi8 = pk.addh(tmp);
+  }
   return p;
 }
 
@@ -472,7 +515,40 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q[q]);
   }
+  for (int v = 0; v < 5; ++v) {
+    const int p = v < 3 ? PREC_F16X3 : (v == 3 ? PREC_F16 : PREC_BF16);
+    h->tcn16_cap[v] = ncu * tcn16_blocks_per_cu(ln, p, v < 3 ? v : 0);
+    h->tcn_cap = std::max(h->tcn_cap, h->tcn16_cap[v]);  // the hand-off words serve either kernel
+  }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
+  // k_tcn16 blobs: per block and GEMM, per (wave, K step of 32) one chunk: the wave's 4 hi tiles, then its lo plane
+  // (fp16: 4 tiles; e4m3 / int8: 2 tile pairs), all in v_mfma_f32_16x16x32 B-fragment order (pack_pointwise g*)
+  for (int v = 0; v < 5; ++v) {
+    const int p = v < 3 ? PREC_F16X3 : (v == 3 ? PREC_F16 : PREC_BF16), lo = v < 3 ? v : 0;
+    const size_t blk = tcn16_block_bytes(p, lo);
+    std::vector<char> bl(blk * h->nblk);
+    for (int i = 0; i < h->nblk; ++i) {
+      char* d = bl.data() + blk * i;
+      for (const PackedW* pw : {&h->blk[i].w1, &h->blk[i].w2}) {
+        const int ns = pw == &h->blk[i].w1 ? CH / 32 : HID / 32;
+        const __half* hi = pk.hblob.data() + (v == 4 ? pw->gbf : pw->ghi);
+        const __half* lp = pk.hblob.data() + (lo == 0 ? pw->glo : (lo == 1 ? pw->gf8 : pw->gi8));
+        for (int w = 0; w < 4; ++w)
+          for (int st = 0; st < ns; ++st) {
+            for (int j = 0; j < 4; ++j, d += 1024) std::memcpy(d, hi + ((size_t)(4 * w + j) * ns + st) * 512, 1024);
+            if (v < 3) {
+              if (lo == 0)
+                for (int j = 0; j < 4; ++j, d += 1024) std::memcpy(d, lp + ((size_t)(4 * w + j) * ns + st) * 512, 1024);
+              else
+                for (int q = 0; q < 2; ++q, d += 1024) std::memcpy(d, lp + ((size_t)(2 * w + q) * ns + st) * 512, 1024);
+            }
+          }
+      }
+      if (d != bl.data() + blk * (i + 1)) { g_err = "k_tcn16 blob layout"; return SEPVAD_E_ARG; }
+    }
+    HIPCHK(hipMalloc(&h->t16w[v], bl.size()));
+    HIPCHK(hipMemcpy(h->t16w[v], bl.data(), bl.size(), hipMemcpyHostToDevice));
+  }
   std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
@@ -535,6 +611,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
 }
 
 void free_ctx(StreamCtx* c) {
+  if (c->done) (void)hipEventDestroy(c->done);
   if (c->ws.base) (void)hipFree(c->ws.base);
   if (c->tgran) (void)hipFree(c->tgran);
   if (c->terr) (void)hipFree(c->terr);
@@ -545,9 +622,8 @@ void free_ctx(StreamCtx* c) {
 int env_int(const char* name, int dflt);
 // The context of caller stream `stream` (created on first use; the caller holds h->mu).
 int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
-  static unsigned long long use_clock = 0;
   for (auto& c : h->ctx)
-    if (c->stream == stream) { c->used = ++use_clock; *out = c.get(); return SEPVAD_OK; }
+    if (c->stream == stream) { c->used = ++h->use_clock; *out = c.get(); return SEPVAD_OK; }
   // cap the per-stream contexts (each holds a workspace, hand-off words and pinned memory): evict the least
   // recently used one after draining its stream (SEPVAD_MAX_STREAM_CTX, default 32)
   const size_t cap = (size_t)std::max(1, env_int("SEPVAD_MAX_STREAM_CTX", 32));
@@ -555,12 +631,13 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
     size_t lru = 0;
     for (size_t i = 1; i < h->ctx.size(); ++i)
       if (h->ctx[i]->used < h->ctx[lru]->used) lru = i;
-    HIPCHK(hipStreamSynchronize((hipStream_t)h->ctx[lru]->stream));
+    HIPCHK(hipEventSynchronize(h->ctx[lru]->done));  // its last enqueued work (not its stream: may be gone)
     free_ctx(h->ctx[lru].release());
     h->ctx.erase(h->ctx.begin() + lru);
   }
   std::unique_ptr<StreamCtx, void (*)(StreamCtx*)> c(new StreamCtx(), free_ctx);
   c->stream = stream;
+  HIPCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   if (h->tcn_cap > 0) {
     const size_t gb = (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long);
     HIPCHK(hipMalloc(&c->tgran, gb));
@@ -575,7 +652,7 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
     const int rc = ws_reserve(c.get(), h->res_B, h->res_N);
     if (rc) return rc;
   }
-  c->used = ++use_clock;
+  c->used = ++h->use_clock;
   *out = c.get();
   h->ctx.emplace_back(c.release());
   return SEPVAD_OK;
@@ -583,7 +660,35 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
 
 // Give-up words written by k_tcn launches of this context that completed since the last check: report
 // each once (the word holds the failing launch's salt, so a later give-up is a new value).
+// n consecutive hand-off tag salts for the k_tcn launches of one forward chunk: never 0, and never wrapping inside
+// the range (k_istft_pair poisons the outputs when the give-up word holds one of gsalt_lo .. gsalt_lo + n - 1). When
+// the 20-bit salt would wrap, the stream is drained and the hand-off words, the device give-up word and its host copy
+// restart from zero (a give-up not yet reported is kept in `pending`), so a reused salt never matches an old word.
+int salt_reserve(sepvad_model* h, StreamCtx* c, hipStream_t s, unsigned n, unsigned* lo) {
+  constexpr unsigned SMAX = (1u << (32 - TCN_EPOCH_BITS)) - 1;
+  const unsigned wrap_at = (unsigned)std::max(2, std::min((int)SMAX, env_int("SEPVAD_TCN_SALT_MAX", (int)SMAX)));
+  if (n > wrap_at) return fail(SEPVAD_E_ARG, "fused TCN: too many launches in one forward");
+  if (c->tsalt + n > wrap_at) {
+    HIPCHK(hipStreamSynchronize(s));
+    const unsigned v = __atomic_load_n(c->herr, __ATOMIC_ACQUIRE);
+    if (v != 0 && v != c->reported) c->pending = v;
+    HIPCHK(hipMemsetAsync(c->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(c->terr, 0, 16, s));
+    __atomic_store_n(c->herr, 0u, __ATOMIC_RELEASE);
+    c->reported = 0;
+    c->tsalt = 0;
+  }
+  *lo = c->tsalt + 1;
+  c->tsalt += n;
+  return SEPVAD_OK;
+}
+
 int check_giveup(StreamCtx* c) {
+  if (c->pending != 0) {
+    c->pending = 0;
+    return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up in an earlier forward on this stream "
+                              "(that forward's outputs are invalid)");
+  }
   const unsigned v = __atomic_load_n(c->herr, __ATOMIC_ACQUIRE);
   if (v != 0 && v != c->reported) {
     c->reported = v;
@@ -870,8 +975,17 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     return nullptr;
   }
   if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
-  if (const char* wl = getenv("SEPVAD_WLO"))  // "i8" (default) | "f16" | "e4m3"
-    h->lo8 = std::strcmp(wl, "e4m3") == 0 ? 1 : (std::strcmp(wl, "f16") == 0 ? 0 : 2);
+  if (const char* t16 = getenv("SEPVAD_TCN16")) h->tcn16 = atoi(t16) != 0;
+  if (const char* wl = getenv("SEPVAD_WLO")) {  // "i8" (default) | "f16" | "e4m3"; anything else is an error
+    if (std::strcmp(wl, "e4m3") == 0) h->lo8 = 1;
+    else if (std::strcmp(wl, "f16") == 0) h->lo8 = 0;
+    else if (std::strcmp(wl, "i8") == 0) h->lo8 = 2;
+    else {
+      g_err = std::string("SEPVAD_WLO: unknown weight lo-plane format '") + wl + "' (expected i8, f16 or e4m3)";
+      sepvad_destroy(h);
+      return nullptr;
+    }
+  }
   if (init_fused(h, pk) != SEPVAD_OK) {
     sepvad_destroy(h);
     return nullptr;
@@ -940,9 +1054,16 @@ int tcn_cap_of(const sepvad_model* h) {
   return h->prec == PREC_F16X3 && h->lo8 ? h->tcn_cap_q[h->lo8] : h->tcn_cap_p[h->prec];
 }
 
+// k_tcn16 (fused16.hip) variant of the current precision / lo plane, and whether it runs at T
+int tcn16_variant(const sepvad_model* h) { return h->prec == PREC_F16X3 ? h->lo8 : (h->prec == PREC_F16 ? 3 : 4); }
+bool use_tcn16(const sepvad_model* h, int T) {
+  const int G = (T + FR16 - 1) / FR16;
+  return h->fused && h->tcn16 && h->prec != PREC_F32 && G <= FG16_MAX && h->tcn16_cap[tcn16_variant(h)] >= G;
+}
+
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G;
+  return use_tcn16(h, T) || (h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G);
 }
 
 int env_int(const char* name, int dflt) {
@@ -1059,23 +1180,28 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
     // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
+    // k_tcn16 (16-frame members, two workgroups per CU) when the utterance fits its groups, else k_tcn
+    const bool t16 = use_tcn16(h, T);
+    const int Gt = t16 ? (T + FR16 - 1) / FR16 : G;  // members per utterance of the kernel that runs
     TcnArgs ta{};
-    ta.T = T; ta.Tp = Tp; ta.G = G; ta.nblk = h->nblk; ta.layer = c.layer;
+    ta.T = T; ta.Tp = Tp; ta.G = Gt; ta.nblk = h->nblk; ta.layer = c.layer;
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
     ta.prec = h->prec;
     ta.lo8 = h->prec == PREC_F16X3 ? h->lo8 : 0;
     ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq[ta.lo8] : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
+    if (t16) ta.wfrag = (const __half*)h->t16w[tcn16_variant(h)];
     ta.prm = h->tprm;
     ta.inv_ch = 1.0 / ((double)CH * T);
     ta.inv_hid = 1.0 / ((double)HID * T);
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
-    auto launch_t = [&](const TcnArgs& t, int grid) { return launch_tcn(t, grid, s); };
+    auto launch_t = [&](const TcnArgs& t, int grid) { return t16 ? launch_tcn16(t, grid, s) : launch_tcn(t, grid, s); };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
-    int ngroups = std::min(B, tcn_cap_of(h) / G);
+    ta.dbg_delay = (unsigned)std::max(0, env_int("SEPVAD_TCN_DELAY", 0));
+    int ngroups = std::min(B, (t16 ? h->tcn16_cap[tcn16_variant(h)] : tcn_cap_of(h)) / Gt);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
     // counted as 4 (headroom)
@@ -1086,38 +1212,34 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
     const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16 * 9;  // wave-0 region + per-wave region
+    // this chunk's launch salts, reserved as one range (salt_reserve: never 0, no wrap inside the range)
+    const bool warm = probe_path && env_int("SEPVAD_TCN_PROBE_WARM", 0);
+    {
+      const int rc = salt_reserve(h, cx, s, (unsigned)((B + per_launch - 1) / per_launch + (warm ? 1 : 0)), &gsalt_lo);
+      if (rc) return rc;
+    }
     gsalt_n = 0;
     for (int u0 = 0; u0 < B; u0 += per_launch) {
       const int Bl = std::min(per_launch, B - u0);
       const int ng = std::min(ngroups, Bl);
       const int ngl = ng >= 8 ? ng - ng % 8 : ng;
-      // tag salt: never 0; hand-off words re-zeroed when the 20-bit salt wraps
-      cx->tsalt = (cx->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
-      if (cx->tsalt == 0) {
-        HIPCHK(hipMemsetAsync(cx->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
-        cx->tsalt = 1;
-      }
-      ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
-      if (gsalt_n++ == 0) gsalt_lo = cx->tsalt;
+      ta.tag0 = (gsalt_lo + gsalt_n++) << TCN_EPOCH_BITS;
       ta.B = Bl;
       ta.S0 = w.S0 + (size_t)u0 * Tp * CH;
       ta.ln = gn_src(w.rec_gate + (size_t)u0 * (Tp / GATE_ROWS) * 2, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
       ta.Xfin = w.O[0] + (size_t)u0 * Tp * CH;
-      ta.rec_head = w.rec_hs + (size_t)u0 * G * 2;
+      ta.rec_head = w.rec_hs + (size_t)u0 * Gt * 2;
       ta.probe = nullptr;
       ta.dump = (h->tdump && u0 == 0 && Bl == B) ? h->tdump : nullptr;
       if (probe_path && u0 == 0) {
         if (!h->tprobe) HIPCHK(hipMalloc(&h->tprobe, probe_n * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(h->tprobe, 0, probe_n * sizeof(unsigned long long), s));
         ta.probe = h->tprobe;
-        if (env_int("SEPVAD_TCN_PROBE_WARM", 0)) {  // diagnostics: an unprobed launch first (warm caches)
+        if (warm) {  // diagnostics: an unprobed launch first (warm caches)
           TcnArgs tw = ta;
           tw.probe = nullptr;
-          HIPCHK(launch_t(tw, ngl * G));
-          cx->tsalt = (cx->tsalt + 1) & ((1u << (32 - TCN_EPOCH_BITS)) - 1);
-          if (cx->tsalt == 0) cx->tsalt = 1;  // (diagnostics: no wrap re-zeroing needed within one forward)
-          ta.tag0 = cx->tsalt << TCN_EPOCH_BITS;
-          ++gsalt_n;
+          HIPCHK(launch_t(tw, ngl * Gt));
+          ta.tag0 = (gsalt_lo + gsalt_n++) << TCN_EPOCH_BITS;
         }
       }
       ta.clk = nullptr;
@@ -1129,8 +1251,11 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         ta.clk = h->tclk + (size_t)(h->tclk_n++ % TCLK_RECS) * 8;
         HIPCHK(hipMemsetAsync(ta.clk, 0, 8 * sizeof(unsigned long long), s));
       }
+      if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
+        fprintf(stderr, "sepvad: %s grid=%d G=%d groups=%d B=%d capacity=%d\n", t16 ? "k_tcn16" : "k_tcn", ngl * Gt, Gt,
+                ngl, Bl, t16 ? h->tcn16_cap[tcn16_variant(h)] : tcn_cap_of(h));
       if (ev()) return SEPVAD_E_HIP;
-      HIPCHK(launch_t(ta, ngl * G));
+      HIPCHK(launch_t(ta, ngl * Gt));
       if (ev()) return SEPVAD_E_HIP;
       if (tr) {
         tr->gemm_ev.push_back((int)h->ev.size() - 2);
@@ -1141,9 +1266,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipMemcpy(hp.data(), h->tprobe, probe_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(probe_path, "wb")) {
-          const long long hdr[4] = {(long long)ngl * G, h->nblk, G, T};
+          const long long hdr[4] = {(long long)ngl * Gt, h->nblk, Gt, T};
           fwrite(hdr, sizeof(hdr), 1, f);
-          const size_t n0 = (size_t)ngl * G * h->nblk * 16;
+          const size_t n0 = (size_t)ngl * Gt * h->nblk * 16;
           fwrite(hp.data(), sizeof(unsigned long long), n0, f);
           fwrite(hp.data() + n0, sizeof(unsigned long long), n0 * 8, f);  // per-wave stamps (kernel layout)
           fclose(f);
@@ -1153,7 +1278,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     // output head on the members' slices (k_head), then the eager masks_b copy if asked
     HeadArgs ha{};
     ha.B = B; ha.T = T; ha.Tp = Tp; ha.G = G; ha.prec = h->prec;
-    ha.Xfin = w.O[0]; ha.rec = w.rec_hs;
+    ha.Xfin = w.O[0]; ha.rec = w.rec_hs; ha.Grec = Gt;
     ha.g = h->P(h->out_g); ha.be = h->P(h->out_b); ha.alpha = h->out_a; ha.sx = h->out_sx;
     ha.inv_ch = 1.0 / ((double)CH * T);
     ha.wh = h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
@@ -1337,7 +1462,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   if (rc) return rc;
   cx->last_B = B;
   cx->last_N = N;
-  ++cx->seq;
+  cx->seq = ++h->fwd_seq;
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   h->ev.clear();
   // diagnostics probe (single chunk only)
@@ -1360,6 +1485,7 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   if (nsplit == 1) {
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     rc = enqueue_chunk(h, cx, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr, xm);
+    HIPCHK(hipEventRecord(cx->done, s));  // (also after a failed enqueue: whatever it queued)
     if (rc) return rc;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
   } else {
@@ -1370,11 +1496,15 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
       const int bc = B / nsplit + (k < B % nsplit ? 1 : 0);
       HIPCHK(hipStreamWaitEvent(h->sub[k], h->fork, 0));
       rc = enqueue_chunk(h, cx, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr, xm);
-      if (rc) return rc;
       HIPCHK(hipEventRecord(h->join[k], h->sub[k]));
       HIPCHK(hipStreamWaitEvent(s, h->join[k], 0));
+      if (rc) {
+        HIPCHK(hipEventRecord(cx->done, s));
+        return rc;
+      }
       b0 += bc;
     }
+    HIPCHK(hipEventRecord(cx->done, s));
   }
   if (h->timing) {
     HIPCHK(hipEventSynchronize(h->ev.back()));
@@ -1518,25 +1648,42 @@ int32_t sepvad_release_stream(sepvad_handle h, void* stream) {
   return SEPVAD_OK;  // nothing held for this stream
 }
 
+}  // extern "C"
+
+namespace {
+// sepvad_side_outputs with h->mu held by the caller (so a check of the forward's identity and the copies it guards
+// are one critical section: no forward can be enqueued on the stream in between)
+int side_outputs_locked(sepvad_model* h, const SepVadOutputs* out, void* stream);
+}  // namespace
+
+extern "C" {
+
 int32_t sepvad_side_outputs_of(sepvad_handle h, const SepVadOutputs* out, void* stream, int64_t seq, int32_t Bx,
                                int32_t Nx) {
   if (!h || !out) return fail(SEPVAD_E_ARG, "sepvad_side_outputs_of: null argument");
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    StreamCtx* cx = nullptr;
-    for (auto& c : h->ctx)
-      if (c->stream == stream) cx = c.get();
-    if (!cx || cx->seq != seq || cx->last_B != Bx || cx->last_N != Nx)
-      return fail(SEPVAD_E_ARG, "side outputs: a later forward on the same stream has replaced the workspace of the "
-                                "forward that produced them (read them before the next forward on that stream)");
-  }
-  return sepvad_side_outputs(h, out, stream);
+  DeviceGuard dg(h->device);
+  std::lock_guard<std::mutex> lk(h->mu);
+  StreamCtx* cx = nullptr;
+  for (auto& c : h->ctx)
+    if (c->stream == stream) cx = c.get();
+  // seq is handle-wide (never reused by a context that was evicted and recreated)
+  if (!cx || cx->seq != seq || cx->last_B != Bx || cx->last_N != Nx)
+    return fail(SEPVAD_E_ARG, "side outputs: a later forward on the same stream has replaced the workspace of the "
+                              "forward that produced them (read them before the next forward on that stream)");
+  return side_outputs_locked(h, out, stream);
 }
 
 int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* stream) {
   if (!h || !out) return fail(SEPVAD_E_ARG, "sepvad_side_outputs: null argument");
   DeviceGuard dg(h->device);
   std::lock_guard<std::mutex> lk(h->mu);
+  return side_outputs_locked(h, out, stream);
+}
+
+}  // extern "C"
+
+namespace {
+int side_outputs_locked(sepvad_model* h, const SepVadOutputs* out, void* stream) {
   StreamCtx* cx = nullptr;
   for (auto& c : h->ctx)
     if (c->stream == stream) cx = c.get();
@@ -1557,8 +1704,12 @@ int32_t sepvad_side_outputs(sepvad_handle h, const SepVadOutputs* out, void* str
     m.B = B; m.T = T; m.Tp = Tp; m.masks = w.masks; m.masks_b = out->masks_b; m.mask = out->mask;
     HIPCHK(launch_mask_side(m, s));
   }
+  HIPCHK(hipEventRecord(cx->done, s));
   return SEPVAD_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int32_t sepvad_stft_gate_test(sepvad_handle h, const float* x, int32_t B, int32_t N, void* X_fm, float* db_fm,
                               void* stream) {
@@ -1581,6 +1732,7 @@ int32_t sepvad_stft_gate_test(sepvad_handle h, const float* x, int32_t B, int32_
   sa.activity = h->cfg.activity_input; sa.gate_w = h->P(h->gate);
   sa.S0 = w.S0; sa.gate_rec = w.rec_gate;
   HIPCHK(launch_stft_gate(sa, (hipStream_t)stream));
+  HIPCHK(hipEventRecord(cx->done, (hipStream_t)stream));
   return SEPVAD_OK;
 }
 
@@ -1757,6 +1909,8 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->twf16) (void)hipFree(h->twf16);
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);
+  for (char* q : h->t16w)
+    if (q) (void)hipFree(q);
   if (h->tprobe) (void)hipFree(h->tprobe);
   if (h->tclk) (void)hipFree(h->tclk);
   if (h->kprobe) (void)hipFree(h->kprobe);

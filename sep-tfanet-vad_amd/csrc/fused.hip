@@ -27,8 +27,9 @@
 // pass in flight together, bounded (a give-up sets *err and the kernel runs to completion instead of
 // hanging). Stores: when all members of a group report the same XCD (HW_REG_XCC_ID, exchanged at epoch
 // 1) plain stores suffice — the XCD's L2 is the coherence point — else agent-scope (sc1) write-through.
-// Slots are double-buffered by epoch parity: every phase consumes a word of every member, so a member
-// writes epoch e+2 only after every member has written e+1, which each does after its epoch-e reads.
+// Slots are double-buffered by epoch parity. A member writes epoch e+2 only after it has polled epoch e+1 of every
+// member, which each wrote after its epoch-e reads -- except where P2 is merged into the P3 round (no poll of its
+// own): there the words of the epochs that could still be read are kept apart by offset (GW_* below).
 //
 // Residency: one 512-thread workgroup per CU (LDS ~158 KB), grid <= the occupancy-derived capacity, and a
 // group's members are dealt to one XCD (blocks b, b+8, ... share an XCD under round-robin dispatch:
@@ -123,13 +124,6 @@ struct TcnSmem {
 static_assert(offsetof(TcnSmem, at) % 8 == 0 && offsetof(TcnSmem, H) % 8 == 0 && offsetof(TcnSmem, prm) % 16 == 0,
               "packed (8-byte) reads of at / H / the parameter blob");
 
-// granule word layout of one slot
-constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq hi}; P4: 11 doubles as 22 words
-constexpr int GW_TOP = 4;           // P1: rows 0..dil-1      [dil][256]
-constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
-constexpr int GW_ROW = 0;           // P3: per-channel sums over own frames [256]
-constexpr int GW_COL = CH;          // P3: per-frame channel sums [32]
-static_assert(GW_BOT + 4 * CH <= NGR, "granule slot size");
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
 template <int PRE, int LQ = 0>
@@ -147,35 +141,6 @@ struct WLay {
 // static register ring; the first PD steps are already in (rh, rl) on entry.
 // PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
 // hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
-// L8 (F16X3 only): the lo plane is e4m3 (sepvad_internal.h WQ_*), one 1 KB wave load per two K steps at
-// voffl + 1024 * pair into rl[i / 2], widened to fp16 in registers (v_cvt_scalef32_pk_f16_fp8, 4 per step,
-// scale 2^-WQ_LO_SHIFT) right before the step's MFMAs: 3 bytes per weight instead of 4.
-// LQ = 2: the lo bytes are int8 steps of 2^-WQ_LO_SHIFT (stored biased, q + 128): v_perm_b32 builds the fp16 values
-// 1024 + byte (0x64XX), and one packed fma scales and unbiases them -- exact (every result is a multiple of 2^-19).
-template <int LQ>
-__device__ __forceinline__ f16x8 lo8_widen(u32x4v q, int half) {
-  constexpr float sc = 1.0f / (float)(1 << WQ_LO_SHIFT);
-  const unsigned d0 = half ? q[2] : q[0], d1 = half ? q[3] : q[1];
-  if constexpr (LQ == 1) {
-    const h16x2 c0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, false);
-    const h16x2 c1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, true);
-    const h16x2 c2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, false);
-    const h16x2 c3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, true);
-    return f16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
-  } else {
-    // v_perm_b32(src0, src1, sel): selector byte k picks byte sel_k of {src0:src1} (0..3 = src1, 4..7 = src0)
-    constexpr unsigned M = 0x64646464u;
-    const h16x2 s2 = {(_Float16)sc, (_Float16)sc}, o2 = {(_Float16)(-1152.0f * sc), (_Float16)(-1152.0f * sc)};
-    h16x2 c[4];
-    c[0] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07010700u));  // bytes 0, 1 -> 0x64b0, 0x64b1
-    c[1] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07030702u));  // bytes 2, 3
-    c[2] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07010700u));
-    c[3] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07030702u));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = __builtin_elementwise_fma(c[k], s2, o2);
-    return f16x8{c[0][0], c[0][1], c[1][0], c[1][1], c[2][0], c[2][1], c[3][0], c[3][1]};
-  }
-}
 
 template <int NS, int LDA, int PRE, int RD = PD, int LQ = 0>
 __device__ __forceinline__ void wave_gemm(f32x16v& acc, const _Float16* Ahi, const _Float16* Alo,
@@ -302,29 +267,6 @@ __device__ __forceinline__ void gn_affine_ch(int tid, const double* acc, int T, 
     }                                                                                              \
   } while (0)
 
-// {sum, sumsq} over the G members' statistic words (member mm: doubles 2mm, 2mm+1 of gw), member order;
-// lanes 0/1 of every wave load and add, the totals are returned wave-uniform
-__device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int lane) {
-  const double* gd = reinterpret_cast<const double*>(gw);
-  const int j = lane & 1;
-  double s = 0.0;
-  for (int mm = 0; mm < G; ++mm) s += gd[2 * mm + j];
-  return double2{readlane_d(s, 0), readlane_d(s, 1)};
-}
-// GroupNorm {mean, rstd} from the statistic words polled by one wave: lane base + 4 mm + {0, 1, 2, 3} holds
-// member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane): the same
-// doubles, in the same order, as member_sums2 over the words in LDS.
-__device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, double inv, float eps, float& mu, float& rs) {
-  double s = 0.0, ss = 0.0;
-  for (int mm = 0; mm < G; ++mm) {
-    const int l = base + 4 * mm;
-    const unsigned a0 = __builtin_amdgcn_readlane(w, l), a1 = __builtin_amdgcn_readlane(w, l + 1);
-    const unsigned b0 = __builtin_amdgcn_readlane(w, l + 2), b1 = __builtin_amdgcn_readlane(w, l + 3);
-    s += __builtin_bit_cast(double, ((u64)a1 << 32) | a0);
-    ss += __builtin_bit_cast(double, ((u64)b1 << 32) | b0);
-  }
-  gn_moments_f(s, ss, inv, eps, mu, rs);
-}
 // Block sums of NV per-thread values (512 threads): waves by DPP, the 8 wave totals in double in wave
 // order by thread j < NV into out[j]. One barrier; callers barrier again before reading `out`.
 template <int NV>
@@ -581,6 +523,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H complete
         if (TCN_SUB == 2) TPROBE(14);
         if (tid < 2) gputd(s1 + GW_STAT + 2 * tid, tag1, sm.dred[tid], l2);
+        tcn_delay(g);  // diagnostics (SEPVAD_TCN_DELAY): member 0 late to its P1 polls
       TPROBE(2);
       }
       // ---- consume P1: neighbours' boundary rows -> H halo; every member's GN1 sums ----
@@ -830,6 +773,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           sm.csum[tid] = s;
           gputf(slot(g, e3) + GW_COL + tid, tag3, s, l2);
         }
+        tcn_delay(g);  // diagnostics (SEPVAD_TCN_DELAY): member 0 late to its P2/P3 polls
       TPROBE(7);
         {
           const u64* pp[FG_CHUNK];
@@ -1145,13 +1089,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(10);
         // ---- P4 words: the moment record (11 doubles); consume every member's ----
         const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
-        if (tid < NMOM) gputd(slot(g, e4) + GW_STAT + 2 * tid, tag4, sm.dred[tid], l2);
+        if (tid < NMOM) gputd(slot(g, e4) + GW_P4 + 2 * tid, tag4, sm.dred[tid], l2);
         {
           // word k % 22 of member k / 22: one word per thread up to 23 members; beyond, passes of up to four words in
           // flight per thread (128 members: 2816 words, two passes)
           const int nw = 2 * NMOM * G;
           if (nw <= NTHR) {
-            const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_STAT + tid % (2 * NMOM) : nullptr};
+            const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_P4 + tid % (2 * NMOM) : nullptr};
             unsigned v[1];
             gpoll<1>(pp, tag4, v, a);
             if (tid < nw) sm.gw[tid] = v[0];
@@ -1161,7 +1105,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int k = k0 + tid + j * NTHR;
-              pp[j] = k < nw ? slot(k / (2 * NMOM), e4) + GW_STAT + k % (2 * NMOM) : nullptr;
+              pp[j] = k < nw ? slot(k / (2 * NMOM), e4) + GW_P4 + k % (2 * NMOM) : nullptr;
             }
             gpoll<4>(pp, tag4, v, a);
 #pragma unroll
@@ -1326,13 +1270,13 @@ __global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
   }
   if (tid < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in order
     double s = 0.0;
-    for (int c0 = 0; c0 < a.G; c0 += FG_CHUNK) {
+    for (int c0 = 0; c0 < a.Grec; c0 += FG_CHUNK) {
       double v[FG_CHUNK];
 #pragma unroll
-      for (int mm = 0; mm < FG_CHUNK; ++mm) v[mm] = c0 + mm < a.G ? a.rec[((size_t)u * a.G + c0 + mm) * 2 + tid] : 0.0;
+      for (int mm = 0; mm < FG_CHUNK; ++mm) v[mm] = c0 + mm < a.Grec ? a.rec[((size_t)u * a.Grec + c0 + mm) * 2 + tid] : 0.0;
 #pragma unroll
       for (int mm = 0; mm < FG_CHUNK; ++mm)
-        if (c0 + mm < a.G) s += v[mm];
+        if (c0 + mm < a.Grec) s += v[mm];
     }
     dred[tid] = s;
   }

@@ -283,7 +283,7 @@ constexpr int FG_MAX = SEPVAD_FG_MAX;  // workgroups per utterance (T <= 4096: 6
                                 // above 32 members span XCDs and hand off through write-through words)
 constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
 constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
-constexpr int NGR = 2112;       // 8-byte {tag, value} hand-off words per slot (>= 4 + 8 * 256)
+constexpr int NGR = 2368;       // 8-byte {tag, value} hand-off words per slot (P1 rows + P3 sums, fused.hip GW_*)
 constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
 constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine
@@ -332,14 +332,23 @@ struct TcnArgs {
                               // (100 MHz wall clock), workgroup 0: start, end wall clock, start, end shader clock}
   float* dump;           // parity probe (sepvad_set_tcn_dump), nullable: [3][B][Tp][CH] = TCN.LN output x'_0,
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
+  unsigned dbg_delay;    // diagnostics (SEPVAD_TCN_DELAY): member 0 of each group sleeps before its polls (0: off)
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
+// The same TCN on 16-frame members, two 256-thread workgroups per CU (fused16.hip k_tcn16); TcnArgs.G counts
+// 16-frame members, wfrag is the k_tcn16 blob (tcn16_block_bytes per block), rec_head [B][G][2]
+constexpr int FR16 = 16;
+constexpr int FG16_MAX = 32;    // members per group (T <= 512); longer utterances run k_tcn
+hipError_t launch_tcn16(const TcnArgs& a, int grid, hipStream_t s);
+int tcn16_blocks_per_cu(int ln_mode, int prec, int lo);
+size_t tcn16_block_bytes(int prec, int lo);
 // Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
 // for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
 struct HeadArgs {
   int B, T, Tp, G, prec;
   const float* Xfin;     // [B][Tp][CH] TCN output x'
-  const double* rec;     // [B][G][2] (sum, sumsq) of PReLU(x') per k_tcn member
+  const double* rec;     // [B][Grec][2] (sum, sumsq) of PReLU(x') per k_tcn / k_tcn16 member
+  int Grec;              // records per utterance (k_tcn: G; k_tcn16: its 16-frame members)
   const float* g; const float* be;  // TCN.output.1 affine
   float alpha;           // TCN.output.0 PReLU
   float sx;              // range scale of the A operand (undone by wscale)

@@ -107,6 +107,51 @@ __device__ __forceinline__ void gpoll(const u64* const (&p)[N], unsigned tag, un
   gpollt<N>(p, tg, v, a);
 }
 
+// Weight lo plane of the fp16x3 split stored as bytes (sepvad_internal.h WQ_*), widened to fp16 in registers:
+// L8 (F16X3 only): the lo plane is e4m3 (sepvad_internal.h WQ_*), one 1 KB wave load per two K steps at
+// voffl + 1024 * pair into rl[i / 2], widened to fp16 in registers (v_cvt_scalef32_pk_f16_fp8, 4 per step,
+// scale 2^-WQ_LO_SHIFT) right before the step's MFMAs: 3 bytes per weight instead of 4.
+// LQ = 2: the lo bytes are int8 steps of 2^-WQ_LO_SHIFT (stored biased, q + 128): v_perm_b32 builds the fp16 values
+// 1024 + byte (0x64XX), and one packed fma scales and unbiases them -- exact (every result is a multiple of 2^-19).
+template <int LQ>
+__device__ __forceinline__ f16x8 lo8_widen(u32x4v q, int half) {
+  constexpr float sc = 1.0f / (float)(1 << WQ_LO_SHIFT);
+  const unsigned d0 = half ? q[2] : q[0], d1 = half ? q[3] : q[1];
+  if constexpr (LQ == 1) {
+    const h16x2 c0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, false);
+    const h16x2 c1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d0, sc, true);
+    const h16x2 c2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, false);
+    const h16x2 c3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(d1, sc, true);
+    return f16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
+  } else {
+    // v_perm_b32(src0, src1, sel): selector byte k picks byte sel_k of {src0:src1} (0..3 = src1, 4..7 = src0)
+    constexpr unsigned M = 0x64646464u;
+    const h16x2 s2 = {(_Float16)sc, (_Float16)sc}, o2 = {(_Float16)(-1152.0f * sc), (_Float16)(-1152.0f * sc)};
+    h16x2 c[4];
+    c[0] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07010700u));  // bytes 0, 1 -> 0x64b0, 0x64b1
+    c[1] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d0, 0x07030702u));  // bytes 2, 3
+    c[2] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07010700u));
+    c[3] = __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(M, d1, 0x07030702u));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = __builtin_elementwise_fma(c[k], s2, o2);
+    return f16x8{c[0][0], c[0][1], c[1][0], c[1][1], c[2][0], c[2][1], c[3][0], c[3][1]};
+  }
+}
+
+// Hand-off word layout of one slot (k_tcn and k_tcn16). With TF-attention a block publishes four epochs (P1, P2, P3, P4), so P1 and P3
+// share a slot parity, as do P2 and P4. P2 is not polled on its own (its words ride in the P3 round), so a member can
+// publish P3 while a slower member still polls its P1 words, and P4 while a slower member still polls its P2 words:
+// P3's words never overlap P1's, and P4's never overlap P2's. Every other same-parity pair is separated by a round
+// that every member polls, which each member enters only after its reads of the earlier epoch.
+constexpr int GW_STAT = 0;          // P1/P2: {sum lo, sum hi, sumsq lo, sumsq hi}
+constexpr int GW_TOP = 4;           // P1: rows 0..dil-1      [dil][256]
+constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
+constexpr int GW_ROW = GW_BOT + 4 * CH;  // P3: per-channel sums over own frames [256]
+constexpr int GW_COL = GW_ROW + CH;      // P3: per-frame channel sums [32]
+constexpr int GW_P4 = 4;                 // P4: the moment record, 11 doubles as 22 words (clear of P2's GW_STAT)
+static_assert(GW_COL + FR <= NGR && GW_P4 >= GW_STAT + 4, "granule slot size / P2-P4 separation");
+
+
 // One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
 // bf16 bits (BF16, round to nearest even) in the hi plane.
 template <int PRE>
@@ -292,6 +337,39 @@ __device__ __forceinline__ KArgs kargs() {
   KArgs p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
   return p;
+}
+
+// {sum, sumsq} over the G members' statistic words (member mm: doubles 2mm, 2mm+1 of gw), member order;
+// lanes 0/1 of every wave load and add, the totals are returned wave-uniform
+__device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int lane) {
+  const double* gd = reinterpret_cast<const double*>(gw);
+  const int j = lane & 1;
+  double s = 0.0;
+  for (int mm = 0; mm < G; ++mm) s += gd[2 * mm + j];
+  return double2{readlane_d(s, 0), readlane_d(s, 1)};
+}
+// GroupNorm {mean, rstd} from the statistic words polled by one wave: lane base + 4 mm + {0, 1, 2, 3} holds
+// member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane): the same
+// doubles, in the same order, as member_sums2 over the words in LDS.
+__device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, double inv, float eps, float& mu, float& rs) {
+  double s = 0.0, ss = 0.0;
+  for (int mm = 0; mm < G; ++mm) {
+    const int l = base + 4 * mm;
+    const unsigned a0 = __builtin_amdgcn_readlane(w, l), a1 = __builtin_amdgcn_readlane(w, l + 1);
+    const unsigned b0 = __builtin_amdgcn_readlane(w, l + 2), b1 = __builtin_amdgcn_readlane(w, l + 3);
+    s += __builtin_bit_cast(double, ((u64)a1 << 32) | a0);
+    ss += __builtin_bit_cast(double, ((u64)b1 << 32) | b0);
+  }
+  gn_moments_f(s, ss, inv, eps, mu, rs);
+}
+
+// Diagnostics (SEPVAD_TCN_DELAY = n): member 0 of every group sleeps n x ~8k cycles at the call sites (after a
+// publish, before the matching polls), so the other members run ahead into the next epochs: the hand-off words of
+// different epochs must not alias while a late member still polls them (fused.hip GW_*). 0 in production.
+__device__ __forceinline__ void tcn_delay(int g) {
+  const unsigned n = kargs()->dbg_delay;
+  if (n != 0 && g == 0)
+    for (unsigned k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(127);
 }
 
 }  // namespace sepvad

@@ -163,6 +163,9 @@ class SeparationModel(nn.Module):
         # storage of the f16x3 weight lo plane in the fused TCN: "i8" (default, 3 B per weight streamed), "f16" or
         # "e4m3" (include/sepvad.h SEPVAD_WLO_*); SEPVAD_WLO overrides
         self.native_weight_lo = os.environ.get("SEPVAD_WLO", "i8")
+        if self.native_weight_lo not in _native.WEIGHT_LO:  # the C layer rejects the same values at create time
+            raise ValueError(f"SEPVAD_WLO: unknown weight lo-plane format {self.native_weight_lo!r} "
+                             f"(expected one of {sorted(_native.WEIGHT_LO)})")
 
     # -- native handle -------------------------------------------------------------------------
     # The handle (folded, packed device weights) is rebuilt lazily after load_state_dict(),

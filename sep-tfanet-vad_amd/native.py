@@ -239,6 +239,8 @@ class Handle:
 
     def set_weight_lo(self, mode: str):
         """Weight lo plane of the fused TCN's f16x3 GEMMs: "i8" (default) / "e4m3" (3 B per weight) or "f16"."""
+        if mode not in WEIGHT_LO:
+            raise ValueError(f"unknown weight lo-plane format {mode!r} (expected one of {sorted(WEIGHT_LO)})")
         _check(self._lib.sepvad_set_weight_lo(self._h, WEIGHT_LO[mode]), "sepvad_set_weight_lo")
         self.weight_lo = mode
 

@@ -274,3 +274,70 @@ def test_shortest_input_and_too_short_input(net, state_dicts):
     with torch.no_grad():  # the handle stays usable after the refused call
         s2, _, _ = net(torch.rand(1, 8000, generator=torch.Generator().manual_seed(1)).to(DEV) * 1.8 - 0.9)
     assert torch.isfinite(s2).all()
+
+
+@pytest.mark.parametrize("B,N", [(64, 32000), (2, 262144)])
+def test_late_member_never_gives_up(net, B, N):
+    """Member 0 of every group sleeps after its P1 and P3 publishes (SEPVAD_TCN_DELAY), so the other members run ahead
+    into the next epochs while it has not yet polled the earlier ones: no hand-off word a late member still polls may
+    be overwritten (fused.hip GW_* layout). No give-up, bitwise the undelayed outputs; G = 4 and G = 33 (cross-XCD)."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(B, N, 515)[0]).to(DEV)
+    ref = {k: v.clone() for k, v in h.forward(x).items() if torch.is_tensor(v)}
+    os.environ["SEPVAD_TCN_DELAY"] = "4"
+    try:
+        out = h.forward(x)
+        assert h.fused_status()
+    finally:
+        del os.environ["SEPVAD_TCN_DELAY"]
+    for k in ("sep", "vad", "est"):
+        assert torch.equal(out[k], ref[k]), k
+
+
+def test_salt_wrap_restarts_giveup_words(net):
+    """SEPVAD_TCN_SALT_MAX=3: the launch salt wraps every third forward. A give-up's salt reused after the wrap must
+    neither poison the later forward (the device give-up word restarts from zero) nor hide a later give-up (the host
+    copy and the reported value restart too); a give-up pending when the salt wraps is still reported once."""
+    g = load_golden("with_vad", "small")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    h = net.native_handle(DEV)
+    s = torch.cuda.Stream()  # a fresh context: salts start at 1 on it
+
+    def fwd(force=False):
+        if force:
+            os.environ["SEPVAD_TCN_FORCE_GIVEUP"] = "1"
+        try:
+            with torch.cuda.stream(s):
+                return h.forward(x)
+        finally:
+            os.environ.pop("SEPVAD_TCN_FORCE_GIVEUP", None)
+
+    os.environ["SEPVAD_TCN_SALT_MAX"] = "3"
+    try:
+        fwd()                      # salt 1
+        bad = fwd(force=True)      # salt 2: gives up
+        torch.cuda.synchronize()
+        assert torch.isnan(bad["sep"]).all()
+        with pytest.raises(RuntimeError, match="gave up"):
+            fwd()
+        fwd()                      # salt 3
+        for _ in range(4):         # wrap; salts 1, 2 (the give-up's), 3, wrap, 1: all valid
+            out = fwd()
+            torch.cuda.synchronize()
+            assert not torch.isnan(out["sep"]).any()
+            assert np.abs(out["sep"].cpu().numpy() - g["sep"]).max() <= SEP_TOL
+        fwd(force=True)            # a give-up just before the next wrap
+        raised = 0
+        for _ in range(3):
+            try:
+                fwd()
+            except RuntimeError as e:
+                assert "gave up" in str(e)
+                raised += 1
+        assert raised == 1
+        torch.cuda.synchronize()
+        assert h.fused_status()
+    finally:
+        del os.environ["SEPVAD_TCN_SALT_MAX"]
+        h.release_stream(s.cuda_stream)

@@ -129,3 +129,13 @@ def test_e4m3_encoder_matches_torch():
     assert lib.sepvad_e4m3_encode((lo * 2 ** 19).ctypes.data, out.ctypes.data, 4096) == 0
     back = torch.from_numpy(out[:4096].copy()).view(torch.float8_e4m3fn).float().numpy() / 2 ** 19
     assert np.all(np.abs(back - lo) <= np.abs(lo) * 2.0 ** -4 + 2.0 ** -29)
+
+
+def test_unknown_weight_lo_is_rejected(monkeypatch):
+    """SEPVAD_WLO is validated in both layers (the C library refuses the same values at sepvad_create)."""
+    import sep_tfanet_vad_amd as pkg
+    monkeypatch.setenv("SEPVAD_WLO", "int8")
+    with pytest.raises(ValueError, match="SEPVAD_WLO"):
+        pkg.SeparationModel(**pkg.CONFIG_WITH_VAD)
+    monkeypatch.setenv("SEPVAD_WLO", "e4m3")
+    assert pkg.SeparationModel(**pkg.CONFIG_WITH_VAD).native_weight_lo == "e4m3"
