@@ -115,6 +115,24 @@ def res_out_bytes(B, T):
     return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
 
 
+STATS_FILE = "r03ab_kernel_stats.csv"    # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
+TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false>"  # the dominant kernel's name in that file
+
+
+def rocprof_avg_us(kernel_prefix):
+    """Average duration (us) of the kernel whose name starts with `kernel_prefix` in the committed rocprofv3 stats of
+    the headline command (profiles/STATS_FILE), so the roofline fraction is reproducible from profiles/ alone."""
+    import csv
+    path = os.path.join(REPO, "profiles", STATS_FILE)
+    try:
+        for r in csv.DictReader(open(path)):
+            if r["Name"].startswith(kernel_prefix):
+                return float(r["AverageNs"]) / 1e3
+    except (OSError, KeyError, ValueError):
+        pass
+    return None
+
+
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
 PMC_FILE_FUSED = "r03ab_pmc_tcn.json"       # fused schedule (k_tcn)
 PMC_WLO = "i8"                             # ... measured with this weight lo plane
@@ -487,6 +505,14 @@ def main():
         }
         if fused:
             out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s, wlo=args.wlo)
+            # the same fraction from the committed rocprofv3 average of the kernel (headline configuration only)
+            if args.precision == "f16x3" and args.wlo == PMC_WLO and B == B_PER_GPU and N == N_SAMPLES:
+                rp = rocprof_avg_us(TCN_KERNEL_PREFIX)
+                if rp:
+                    out["roofline"]["rocprof"] = {"avg_launch_us": round(rp, 2),
+                                                  "achieved": round(flops_launch / (rp * 1e-6) / 1e12, 3),
+                                                  "frac": round(flops_launch / (rp * 1e-6) / 1e12 / peak, 4),
+                                                  "source": "profiles/" + STATS_FILE}
         if world == 1 and not args.no_cpu_baseline and args.workload == "offline":
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         emit(out)

@@ -167,6 +167,7 @@ struct sepvad_model {
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
   // k_tcn16 (fused16.hip: 16-frame members, two workgroups per CU) for T <= 16 * FG16_MAX; opt-in (SEPVAD_TCN16=1)
   bool tcn16 = false;
+  int t16_waves = 8;            // waves per k_tcn16 workgroup (SEPVAD_TCN16_WAVES=4|8; the blob layout follows)
   char* t16w[5] = {};           // [nblk][tcn16_block_bytes] blobs: [0..2] F16X3 with the fp16 / e4m3 / int8 lo plane, [3] F16, [4] BF16
   int tcn16_cap[5] = {};        // co-resident k_tcn16 workgroups per variant
   bool last_fused = false;
@@ -517,7 +518,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   }
   for (int v = 0; v < 5; ++v) {
     const int p = v < 3 ? PREC_F16X3 : (v == 3 ? PREC_F16 : PREC_BF16);
-    h->tcn16_cap[v] = ncu * tcn16_blocks_per_cu(ln, p, v < 3 ? v : 0);
+    h->tcn16_cap[v] = ncu * tcn16_blocks_per_cu(ln, p, v < 3 ? v : 0, h->t16_waves);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn16_cap[v]);  // the hand-off words serve either kernel
   }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
@@ -533,14 +534,16 @@ int init_fused(sepvad_model* h, const Packer& pk) {
         const int ns = pw == &h->blk[i].w1 ? CH / 32 : HID / 32;
         const __half* hi = pk.hblob.data() + (v == 4 ? pw->gbf : pw->ghi);
         const __half* lp = pk.hblob.data() + (lo == 0 ? pw->glo : (lo == 1 ? pw->gf8 : pw->gi8));
-        for (int w = 0; w < 4; ++w)
+        const int nw = h->t16_waves, tpw = 16 / nw;  // waves, 16-channel tiles per wave
+        for (int w = 0; w < nw; ++w)
           for (int st = 0; st < ns; ++st) {
-            for (int j = 0; j < 4; ++j, d += 1024) std::memcpy(d, hi + ((size_t)(4 * w + j) * ns + st) * 512, 1024);
+            for (int j = 0; j < tpw; ++j, d += 1024) std::memcpy(d, hi + ((size_t)(tpw * w + j) * ns + st) * 512, 1024);
             if (v < 3) {
               if (lo == 0)
-                for (int j = 0; j < 4; ++j, d += 1024) std::memcpy(d, lp + ((size_t)(4 * w + j) * ns + st) * 512, 1024);
+                for (int j = 0; j < tpw; ++j, d += 1024) std::memcpy(d, lp + ((size_t)(tpw * w + j) * ns + st) * 512, 1024);
               else
-                for (int q = 0; q < 2; ++q, d += 1024) std::memcpy(d, lp + ((size_t)(2 * w + q) * ns + st) * 512, 1024);
+                for (int q = 0; q < tpw / 2; ++q, d += 1024)
+                  std::memcpy(d, lp + ((size_t)(tpw / 2 * w + q) * ns + st) * 512, 1024);
             }
           }
       }
@@ -976,6 +979,7 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
   }
   if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
   if (const char* t16 = getenv("SEPVAD_TCN16")) h->tcn16 = atoi(t16) != 0;
+  if (const char* t16w = getenv("SEPVAD_TCN16_WAVES")) h->t16_waves = atoi(t16w) == 4 ? 4 : 8;
   if (const char* wl = getenv("SEPVAD_WLO")) {  // "i8" (default) | "f16" | "e4m3"; anything else is an error
     if (std::strcmp(wl, "e4m3") == 0) h->lo8 = 1;
     else if (std::strcmp(wl, "f16") == 0) h->lo8 = 0;
@@ -1185,6 +1189,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     const int Gt = t16 ? (T + FR16 - 1) / FR16 : G;  // members per utterance of the kernel that runs
     TcnArgs ta{};
     ta.T = T; ta.Tp = Tp; ta.G = Gt; ta.nblk = h->nblk; ta.layer = c.layer;
+    if (const int nb = env_int("SEPVAD_TCN_NBLK", 0); nb > 0 && nb < h->nblk) ta.nblk = nb;  // diagnostics: truncated stack
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
     ta.prec = h->prec;
@@ -1197,10 +1202,13 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
-    auto launch_t = [&](const TcnArgs& t, int grid) { return t16 ? launch_tcn16(t, grid, s) : launch_tcn(t, grid, s); };
+    auto launch_t = [&](const TcnArgs& t, int grid) {
+      return t16 ? launch_tcn16(t, grid, h->t16_waves, s) : launch_tcn(t, grid, s);
+    };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     ta.dbg_delay = (unsigned)std::max(0, env_int("SEPVAD_TCN_DELAY", 0));
+    ta.dump_blk = std::max(0, std::min(h->nblk - 1, env_int("SEPVAD_TCN_DUMP_BLOCK", 0)));
     int ngroups = std::min(B, (t16 ? h->tcn16_cap[tcn16_variant(h)] : tcn_cap_of(h)) / Gt);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;

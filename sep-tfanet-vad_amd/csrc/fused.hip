@@ -436,6 +436,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int m = mo_, tid = tido, lane = tid & 63, hl = hl4o >> 2, wave = wave_s;
       auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4o; };
       TPROBE(0);
+      if (DUMP && bi > 0 && bi == kargs()->dump_blk) {  // parity probe (SEPVAD_TCN_DUMP_BLOCK): this block's input
+        if (float* dp = kargs()->dump) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dp[((size_t)u * Tp + t0 + trow(r)) * CH + m] = o[r];
+        }
+      }
       if (TP_ON && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
         a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
       const __half* wb = a.wfrag + (size_t)bi * WL::BLOCK;
@@ -995,7 +1001,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // ---- residual update (model/model.py:345-352) ----
       // gate r in place once: r' = r a_f a_t (a_f = a_t = 1 without TF-attention, set at kernel start)
       {
-        if (bi == 0) {  // parity probe: DepthConv1d output of block 0 (model/model.py:144), before the gates
+        if (bi == kargs()->dump_blk) {  // parity probe: DepthConv1d output of block 0 (model/model.py:144), before the gates
           if (float* dp = DUMP ? kargs()->dump : nullptr) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) dp[((size_t)(kargs()->B + u) * Tp + t0 + trow(r)) * CH + m] = rv[r];
@@ -1013,7 +1019,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) rv[r] = rv[r] * (afm * sm.at[trow(r)]);
 #endif
-        if (bi == 0) {  // parity probe: TF_Attention output of block 0 (model/model.py:207)
+        if (bi == kargs()->dump_blk) {  // parity probe: TF_Attention output of block 0 (model/model.py:207)
           if (float* dp = DUMP ? kargs()->dump : nullptr) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) dp[((size_t)(2 * kargs()->B + u) * Tp + t0 + trow(r)) * CH + m] = rv[r];

@@ -30,15 +30,24 @@ namespace t16 {
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int F = FR16;            // frames per member
-constexpr int NT = 256;            // 4 waves per workgroup
-constexpr int NW = NT / 64;
 constexpr int LDX = CH + 8;        // x' row stride (halves): 132 dwords == 4 (mod 64): conflict-free 16-row b128 reads
 constexpr int LDD = HID + 8;       // d row stride (halves): 260 dwords == 4 (mod 64)
 constexpr int HR = F + 8;          // conv1d output rows incl. 4 halo rows on each side
 constexpr int NS1 = CH / 32;       // conv1d K steps of 32
 constexpr int NS2 = HID / 32;      // res_out K steps of 32
 constexpr int GMAX = FG16_MAX;     // members per group
-constexpr int PCH = 16;            // members' P3 row sums polled per pass
+// Workgroup geometry by wave count NWV (4 or 8): wave w owns output channels [CPW w, CPW w + CPW) as TPW tiles of 16
+template <int NWV>
+struct Geo {
+  static constexpr int NW = NWV, NT = 64 * NWV;
+  static constexpr int TPW = 16 / NWV;      // 16-channel tiles per wave
+  static constexpr int CPW = 16 * TPW;      // channels per wave
+  static constexpr int VPT = 4 * TPW;       // residual values per thread (4 frames x TPW channels)
+  static constexpr int KH = 2048 / NT;      // P1 halo words per thread (2 x dil x 256 <= 2048)
+  static constexpr int FPT = F * (CH / 2) / NT;  // depthwise frames per thread (input-channel pairs x frame slices)
+  static constexpr int PCH = NWV == 4 ? 16 : 8;  // members' P3 row sums polled per pass
+  static constexpr int WPE = NWV / 2;       // waves per SIMD at two workgroups per CU (launch bound)
+};
 // parameter blob staged in LDS: floats [0, PB_WD) (conv1d epilogue, GN1 affine) and [PB_WS2, PB_SIZE) (res_out
 // epilogue, LN affines, attention taps, scalars); the depthwise weights (PB_WD .. PB_WS2) are read from global
 constexpr int PS1 = PB_WD, PS2 = PB_SIZE - PB_WS2, PSTAGE = PS1 + PS2;
@@ -49,7 +58,9 @@ static_assert((PB_WSUM - (PB_WS2 - PS1)) % 2 == 0, "8-byte alignment of the stag
 #define TCN16_RD 2   // weight K steps (of 32) in flight per wave (4: 256 VGPRs + 6 spilled)
 #endif
 
+template <int NWV>
 struct Smem {
+  static constexpr int NW = NWV;
   _Float16 Ahi[F * LDD];           // GEMM A operand, hi plane: x' [16][LDX] or d [16][LDD]
   _Float16 Alo[F * LDD];           //                 lo plane
   float H[HR * CH];                // conv1d output (raw, pre-GN1) rows -4..19; the attention vectors alias it
@@ -63,42 +74,47 @@ struct Smem {
   unsigned gw[2 * NMOM * GMAX] __attribute__((aligned(8)));  // gathered statistic words of all members
   double dred[16];
 };
-static_assert(offsetof(Smem, H) % 16 == 0 && offsetof(Smem, prm) % 16 == 0 && offsetof(Smem, at) % 8 == 0, "alignment");
-static_assert(sizeof(Smem) <= 80 * 1024, "two workgroups per CU (160 KB LDS)");
+static_assert(offsetof(Smem<4>, H) % 16 == 0 && offsetof(Smem<4>, prm) % 16 == 0 && sizeof(Smem<4>) <= 80 * 1024 &&
+              offsetof(Smem<8>, H) % 16 == 0 && offsetof(Smem<8>, prm) % 16 == 0 && sizeof(Smem<8>) <= 80 * 1024,
+              "alignment; two workgroups per CU (160 KB LDS)");
 
 // A staged parameter (blob index i, PB_*)
-__device__ __forceinline__ const float* P(const Smem& sm, int i) { return sm.prm + (i < PS1 ? i : i - (PB_WS2 - PS1)); }
+template <class S>
+__device__ __forceinline__ const float* P(const S& sm, int i) { return sm.prm + (i < PS1 ? i : i - (PB_WS2 - PS1)); }
 
-// Weight-blob geometry per operand format: per (wave, K step) one contiguous chunk of SB bytes: the 4 hi tiles
-// (1 KB each), then the lo plane (fp16: 4 tiles; e4m3 / int8: 2 tile pairs of 1 KB).
-template <int PRE, int LQ>
+// Weight-blob geometry per operand format: per (wave, K step) one contiguous chunk of SB bytes: the wave's TPW hi
+// tiles (1 KB each), then its lo plane (fp16: TPW tiles; e4m3 / int8: TPW / 2 tile pairs of 1 KB).
+template <int PRE, int LQ, int NWV>
 struct Lay {
+  static constexpr int TPW = Geo<NWV>::TPW, NW = NWV;
   static constexpr bool X3 = PRE == PREC_F16X3, L8 = LQ != 0;
-  static constexpr int NLO = X3 ? (L8 ? 2 : 4) : 0;
+  static constexpr int NLO = X3 ? (L8 ? TPW / 2 : TPW) : 0;
   static constexpr int NLO1 = NLO > 0 ? NLO : 1;
-  static constexpr int SB = 4096 + 1024 * NLO;                  // bytes per (wave, step)
+  static constexpr int SB = 1024 * TPW + 1024 * NLO;            // bytes per (wave, step)
   static constexpr size_t W1 = 0, W2 = (size_t)NW * NS1 * SB;   // byte offsets of the two GEMMs in a block
-  static constexpr size_t BLOCK = (size_t)NW * (NS1 + NS2) * SB;  // bytes per block
+  static constexpr size_t BLOCK = (size_t)NW * (NS1 + NS2) * SB;  // bytes per block (the same for 4 and 8 waves)
 };
 
-// ring entry i <- K step s (4 hi tiles + the lo plane of step s)
-template <int PRE, int LQ, int RD>
-__device__ __forceinline__ void ring_load(__amdgpu_buffer_rsrc_t w, int voff, u32x4v (&rh)[RD][4],
-                                          u32x4v (&rl)[RD][Lay<PRE, LQ>::NLO1], int i, int s) {
-  using L = Lay<PRE, LQ>;
+// ring entry i <- K step s (the TPW hi tiles + the lo plane of step s)
+template <int PRE, int LQ, int NWV, int RD>
+__device__ __forceinline__ void ring_load(__amdgpu_buffer_rsrc_t w, int voff, u32x4v (&rh)[RD][Geo<NWV>::TPW],
+                                          u32x4v (&rl)[RD][Lay<PRE, LQ, NWV>::NLO1], int i, int s) {
+  using L = Lay<PRE, LQ, NWV>;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) rh[i][j] = __builtin_amdgcn_raw_buffer_load_b128(w, voff, s * L::SB + 1024 * j, 0);
+  for (int j = 0; j < L::TPW; ++j) rh[i][j] = __builtin_amdgcn_raw_buffer_load_b128(w, voff, s * L::SB + 1024 * j, 0);
 #pragma unroll
-  for (int p = 0; p < L::NLO; ++p) rl[i][p] = __builtin_amdgcn_raw_buffer_load_b128(w, voff, s * L::SB + 4096 + 1024 * p, 0);
+  for (int p = 0; p < L::NLO; ++p)
+    rl[i][p] = __builtin_amdgcn_raw_buffer_load_b128(w, voff, s * L::SB + 1024 * L::TPW + 1024 * p, 0);
 }
 
 // acc[j] (16 frames x channels 16j.. of the wave) += A[16 x 32 NS] . W^T on v_mfma_f32_16x16x32; A from LDS (row
 // stride LDA halves), the weight steps stream through a static register ring of RD steps (the first RD already in)
-template <int NS, int LDA, int PRE, int LQ, int RD>
-__device__ __forceinline__ void wave_gemm(f32x4v (&acc)[4], const _Float16* Ahi, const _Float16* Alo,
-                                          __amdgpu_buffer_rsrc_t w, int voff, u32x4v (&rh)[RD][4],
-                                          u32x4v (&rl)[RD][Lay<PRE, LQ>::NLO1], int lane) {
-  using L = Lay<PRE, LQ>;
+template <int NS, int LDA, int PRE, int LQ, int NWV, int RD>
+__device__ __forceinline__ void wave_gemm(f32x4v (&acc)[Geo<NWV>::TPW], const _Float16* Ahi, const _Float16* Alo,
+                                          __amdgpu_buffer_rsrc_t w, int voff, u32x4v (&rh)[RD][Geo<NWV>::TPW],
+                                          u32x4v (&rl)[RD][Lay<PRE, LQ, NWV>::NLO1], int lane) {
+  using L = Lay<PRE, LQ, NWV>;
+  constexpr int TP = L::TPW;
   constexpr bool X3 = L::X3, L8 = L::L8;
   static_assert(NS % RD == 0 && NS >= RD, "K steps");
   const int aoff = (lane & 15) * LDA + 8 * (lane >> 4);
@@ -115,35 +131,35 @@ __device__ __forceinline__ void wave_gemm(f32x4v (&acc)[4], const _Float16* Ahi,
     }
     const f16x8 ah = aH[cur], al = aL[cur];
     if constexpr (X3) {
-      f16x8 bh[4], bl[4];
+      f16x8 bh[TP], bl[TP];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TP; ++j) {
         bh[j] = __builtin_bit_cast(f16x8, rh[i][j]);
         if constexpr (L8) bl[j] = lo8_widen<LQ>(rl[i][j >> 1], j & 1);
         else bl[j] = __builtin_bit_cast(f16x8, rl[i][j]);
       }
       // four independent accumulators between dependent MFMAs
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[j], 0, 0, 0);
+      for (int j = 0; j < TP; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[j], 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[j], 0, 0, 0);
+      for (int j = 0; j < TP; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[j], 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[j], 0, 0, 0);
+      for (int j = 0; j < TP; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[j], 0, 0, 0);
     } else if constexpr (PRE == PREC_F16) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TP; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, rh[i][j]), acc[j], 0, 0, 0);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TP; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, rh[i][j]),
                                                          acc[j], 0, 0, 0);
     }
-    if (pf) ring_load<PRE, LQ, RD>(w, voff, rh, rl, i, s + RD);
+    if (pf) ring_load<PRE, LQ, NWV, RD>(w, voff, rh, rl, i, s + RD);
     // pipeline shape of a step: the next step's A reads (DS), this step's MFMAs, then the ring refill (VMEM)
     if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, X3 ? 2 : 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 12 : 4, 0);
-    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, 4 + L::NLO, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 3 * TP : TP, 0);
+    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, TP + L::NLO, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
 #pragma unroll
@@ -157,7 +173,7 @@ __device__ __forceinline__ void wave_gemm(f32x4v (&acc)[4], const _Float16* Ahi,
 
 // Block sums of NV per-thread floats (4 waves): waves by DPP, the wave totals in double in wave order by thread
 // j < NV into out[j] (LDS or global). One barrier; callers barrier again before reading an LDS `out`.
-template <int NV>
+template <int NV, int NW>
 __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* out) {
   const int w = threadIdx.x >> 6;
   float t[NV];
@@ -201,18 +217,26 @@ __device__ __forceinline__ float row_total(float v) {
     }                                                                                                \
   } while (0)
 
-template <int LM, int PRE, bool DUMP = false, int LQ = 0, bool PROBE = false>
-__global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
-  using L = Lay<PRE, LQ>;
+template <int LM, int PRE, int NWV, bool DUMP = false, int LQ = 0, bool PROBE = false>
+__global__ __launch_bounds__(64 * NWV, NWV / 2) void k_tcn16(TcnArgs a) {
+  using GE = Geo<NWV>;
+  using L = Lay<PRE, LQ, NWV>;
+  constexpr int NT = GE::NT, NW = GE::NW, TPW = GE::TPW, CPW = GE::CPW, VPT = GE::VPT, KH = GE::KH, FPT = GE::FPT;
+  constexpr int PCH = GE::PCH;
   constexpr int RD = TCN16_RD;
-  static_assert(8 % RD == 0, "ring entries spread over the 8 rows of the phases before the GEMMs");
-  constexpr int RS = 8 / RD;  // rows per ring entry in those phases
-  __shared__ __attribute__((aligned(16))) Smem sm;
+  static_assert(FPT % RD == 0 && (2 * TPW) % RD == 0, "ring entries spread over the rows of the phases before the GEMMs");
+  constexpr int RS = FPT / RD;       // depthwise frames per res_out ring entry
+  constexpr int RX = 2 * TPW / RD;   // x' row pairs per conv1d ring entry
+  __shared__ __attribute__((aligned(16))) Smem<NWV> sm;
   const int tid = threadIdx.x;
   const int wave_s = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = a.G;
   int grp, g;  // members of a group on one XCD when the grid is a multiple of 8 G (speed only)
-  if (gridDim.x % (8 * G) == 0) {
+  if (a.xmode >= 2 && gridDim.x % (8 * G) == 0) {  // diagnostics: consecutive workgroups of an XCD in different groups
+    const int x = blockIdx.x & 7, idx = blockIdx.x >> 3, gpx = gridDim.x / (8 * G);  // groups per XCD
+    grp = (idx % gpx) * 8 + x;
+    g = idx / gpx;
+  } else if (gridDim.x % (8 * G) == 0) {
     const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
     grp = (idx / G) * 8 + x;
     g = idx % G;
@@ -236,7 +260,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
     if (blockIdx.x == 0) { a.clk[2] = rt; a.clk[4] = __builtin_amdgcn_s_memtime(); }
   }
   if (!a.tf_att) {  // no TF-attention: unit gates
-    sm.af[tid] = 1.f;
+    if (tid < CH) sm.af[tid] = 1.f;
     if (tid < F) sm.at[tid] = 1.f;
   }
   bool l2 = false;
@@ -245,12 +269,12 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
   const int voff = (tid & 63) * 16;  // this lane's 16 bytes of a 1 KB wave fragment
 
   for (int u = grp; u < a.B; u += ngroups) {
-    float o[16];  // o[4j + i]: frame 4(l>>4) + i, channel 64 wave + 16 j + (l & 15)
-    u32x4v rh[RD][4], rl[RD][L::NLO1];
+    float o[VPT];  // o[4j + i]: frame 4(l>>4) + i, channel CPW wave + 16 j + (l & 15)
+    u32x4v rh[RD][TPW], rl[RD][L::NLO1];
     {
       const int tidu = fresh_tid(wave_s);
-      const int f0 = 4 * ((tidu & 63) >> 4), ch = 64 * wave_s + (tidu & 15);
-      float raw[16], pg[4], pb[4], sx0;
+      const int f0 = 4 * ((tidu & 63) >> 4), ch = CPW * wave_s + (tidu & 15);
+      float raw[VPT], pg[TPW], pb[TPW], sx0;
       {
         const KArgs ka = kargs();
         const __amdgpu_buffer_rsrc_t s0r = rsrc_of(ka->S0 + ((size_t)u * Tp + t0) * CH);
@@ -259,18 +283,18 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         const int vo = (f0 * CH + ch) * 4;
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)  // rows < G * 16 <= Tp: in bounds (masked below)
             raw[4 * j + i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(s0r, vo, (i * CH + 16 * j) * 4, 0));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           pg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, (ch + 16 * j) * 4, 0, 0));
           pb[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ber, (ch + 16 * j) * 4, 0, 0));
         }
         sx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc_of(ka->prm), 0, PB_SX * 4, 0));
 #pragma unroll
-        for (int i = 0; i < RD; ++i) ring_load<PRE, LQ, RD>(w1, voff, rh, rl, i, i);  // block-0 conv1d weights
+        for (int i = 0; i < RD; ++i) ring_load<PRE, LQ, NWV, RD>(w1, voff, rh, rl, i, i);  // block-0 conv1d weights
         __builtin_amdgcn_sched_barrier(0);
       }
       reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
@@ -282,7 +306,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         gpoll<1>(p, a.tag0 + 1, v, a);
         if (tid < G) sm.gw[tid] = v[0];
         __syncthreads();
-        bool same = a.xmode == 0;
+        bool same = a.xmode == 0 || a.xmode == 2;
         for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
         l2 = same;
       }
@@ -291,7 +315,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
       float mu, rs;
       gn_moments(sm.dred[0], sm.dred[1], (double)CH * T, a.ln.eps, mu, rs);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TPW; ++j) {
         const float sc = rs * pg[j], sh = pb[j] - sc * mu;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[4 * j + i] = fmaf(raw[4 * j + i], sc, sh) * (t0 + f0 + i < T ? 1.f : 0.f);
@@ -302,7 +326,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
       }
       if (float* dp = DUMP ? kargs()->dump : nullptr) {  // parity probe: TCN.LN output (model/model.py:333)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) dp[((size_t)u * Tp + t0 + f0 + i) * CH + ch + 16 * j] = o[4 * j + i];
       }
@@ -311,44 +335,54 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
     for (int bi = 0; bi < a.nblk; ++bi) {
       // opaque per-iteration thread coordinates (fused.hip: keeps hipcc from hoisting per-row addresses)
       const int tido = fresh_tid(wave_s);
-      const int tid = tido, lane = tid & 63, f0 = 4 * (lane >> 4), ch = 64 * wave_s + (lane & 15);
+      const int tid = tido, lane = tid & 63, f0 = 4 * (lane >> 4), ch = CPW * wave_s + (lane & 15);
       const bool odd = (lane & 1) != 0;
       auto fm = [&](int i) { return t0 + f0 + i < T ? 1.f : 0.f; };  // own frame f0 + i valid
       const char* wb = reinterpret_cast<const char*>(a.wfrag) + (size_t)bi * L::BLOCK;
       const int li = bi % a.layer;
       const int dil = li == 0 ? 1 : (li % 4 + 1);  // model/model.py:285-295 (as api.hip packs it)
       // this block's staged parameters: loads now, LDS stores after the conv1d GEMM
-      u32x4v pv[3];
+      constexpr int NPV = (PSTAGE / 4 + NT - 1) / NT;
+      u32x4v pv[NPV];
       {
         const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(uni(a.prm + (size_t)bi * PB_SIZE)), (short)0, PB_SIZE * 4, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int q = tid + k * NT;  // float4 index of the staged blob
+        for (int k = 0; k < NPV; ++k) {
+          const int q = tid + k * NT;  // float4 index of the staged blob (past its end: the buffer reads 0)
           pv[k] = __builtin_amdgcn_raw_buffer_load_b128(pr, (q < PS1 / 4 ? q : q + (PB_WS2 - PS1) / 4) * 16, 0, 0);
         }
       }
       const float* pgl = a.prm + (size_t)bi * PB_SIZE;
-      float ws1[4], b1[4];
+      float ws1[TPW], b1[TPW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { ws1[j] = pgl[PB_WS1 + ch + 16 * j]; b1[j] = pgl[PB_B1 + ch + 16 * j]; }
+      for (int j = 0; j < TPW; ++j) { ws1[j] = pgl[PB_WS1 + ch + 16 * j]; b1[j] = pgl[PB_B1 + ch + 16 * j]; }
       const float a1 = unif(pgl[PB_A1]);
       const unsigned e1 = ++ep, tag1 = a.tag0 + e1;
       T16P(0);
-      // ================= conv1d 256->256 (model/model.py:132) + PReLU =================
-      f32x4v acc[4];
+      if (DUMP && bi > 0 && bi == kargs()->dump_blk) {  // parity probe (SEPVAD_TCN_DUMP_BLOCK): this block's input
+        if (float* dp = kargs()->dump) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      wave_gemm<NS1, LDX, PRE, LQ, RD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + L::W1 + (size_t)wave_s * NS1 * L::SB), voff, rh, rl,
-                                       lane);
+          for (int j = 0; j < TPW; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dp[((size_t)u * Tp + t0 + f0 + i) * CH + ch + 16 * j] = o[4 * j + i];
+        }
+      }
+      // ================= conv1d 256->256 (model/model.py:132) + PReLU =================
+      f32x4v acc[TPW];
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      wave_gemm<NS1, LDX, PRE, LQ, NWV, RD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + L::W1 + (size_t)wave_s * NS1 * L::SB), voff, rh,
+                                            rl, lane);
       T16P(1);
       // depthwise parameters of this thread's input-channel pair (not staged): in flight through the epilogue and P1
-      const int c2 = 2 * (tid & (CH / 2 - 1)), fr0 = (tid >> 7) * (F / 2);
+      // (4 waves; with 8 the registers are short, and they are loaded after the P1 round)
+      const int c2 = 2 * (tid & (CH / 2 - 1)), fr0 = (tid >> 7) * FPT;
       f32x2 wv[2][3], bv[2];
-      dw_params2(pgl, c2, wv, bv);
+      if constexpr (NWV == 4) dw_params2(pgl, c2, wv, bv);
       {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < NPV; ++k) {
           const int q = tid + k * NT;
           if (q < PSTAGE / 4) reinterpret_cast<u32x4v*>(sm.prm)[q] = pv[k];
         }
@@ -356,7 +390,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         f32x2 s0 = {0.f, 0.f}, q0 = {0.f, 0.f};
         const float a1m1 = a1 - 1.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           const int c = ch + 16 * j;
 #pragma unroll
           for (int i = 0; i < 4; i += 2) {
@@ -376,18 +410,18 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           }
         }
         float st[2] = {s0.x + s0.y, q0.x + q0.y};
-        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: H and the staged blob complete
+        block_sums<2, NW>(st, sm.red, sm.dred);  // barrier inside: H and the staged blob complete
         if (tid < 2) gputd(s1 + GW_STAT + 2 * tid, tag1, sm.dred[tid], l2);
         tcn_delay(g);  // diagnostics (SEPVAD_TCN_DELAY)
         T16P(2);
       }
       // ---- consume P1: neighbours' boundary rows -> H halo; every member's GN1 sums ----
       {
-        const u64* p[9];
-        unsigned v[9];
-        int hrow[8], hcol[8];
+        const u64* p[KH + 1];
+        unsigned v[KH + 1];
+        int hrow[KH], hcol[KH];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < KH; ++k) {
           const int i = tid + k * NT;
           p[k] = nullptr;
           hrow[k] = -1; hcol[k] = 0;
@@ -404,25 +438,26 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           }
         }
         const int sk = tid - (NT - 4 * G);  // last 4G threads: GN1 words of member sk/4
-        p[8] = sk >= 0 ? slot(sk >> 2, e1) + GW_STAT + (sk & 3) : nullptr;
-        gpoll<9>(p, tag1, v, a);
+        p[KH] = sk >= 0 ? slot(sk >> 2, e1) + GW_STAT + (sk & 3) : nullptr;
+        gpoll<KH + 1>(p, tag1, v, a);
         T16P(3);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
+        for (int k = 0; k < KH; ++k)
           if (hrow[k] >= 0) sm.H[hrow[k] * CH + hcol[k]] = p[k] != nullptr ? __builtin_bit_cast(float, v[k]) : 0.f;
         if (G <= FG_WAVE) {
           if (wave_s == NW - 1) {  // the GN1 pollers' wave: moments before the barrier
             float mu, rs;
-            member_moments_w(v[8], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
+            member_moments_w(v[KH], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
             if (lane == 0) { sm.gmom[0] = mu; sm.gmom[1] = rs; }
           }
         } else if (sk >= 0) {
-          sm.gw[sk] = v[8];
+          sm.gw[sk] = v[KH];
         }
         __syncthreads();  // halo rows and the GN1 moments / words in LDS
       }
       // ================= depthwise conv (model/model.py:134-135): d = PReLU(dconv(GN1(h))) =================
       {
+        if constexpr (NWV != 4) dw_params2(pgl, c2, wv, bv);
         float mu, rs;
         if (G <= FG_WAVE) {
           mu = sm.gmom[0]; rs = sm.gmom[1];
@@ -435,21 +470,21 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         const f32x2 sh2 = *reinterpret_cast<const f32x2*>(P(sm, PB_BE1 + c2)) - sc2 * mu;
         const float a2m1 = *P(sm, PB_A2) - 1.f;
         f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
-        // thread = input channels c2, c2+1 (hidden 2c2..2c2+3) x frames fr0..fr0+7; rows fr0-D .. fr0+7+D once into
-        // registers (GN1 applied, zero outside [0, T)); H holds rows -4..F+3, so every load is in bounds
+        // thread = input channels c2, c2+1 (hidden 2c2..2c2+3) x frames fr0..fr0+FPT-1; rows fr0-D .. fr0+FPT-1+D once
+        // into registers (GN1 applied, zero outside [0, T)); H holds rows -4..F+3, so every load is in bounds
         auto rows = [&](auto DC) {
           constexpr int D = decltype(DC)::value;
           const float* hb = lds_base(sm.H + (fr0 - D + 4) * CH + c2);
-          f32x2 hv[F / 2 + 2 * D];
+          f32x2 hv[FPT + 2 * D];
 #pragma unroll
-          for (int i = 0; i < F / 2 + 2 * D; ++i) {
+          for (int i = 0; i < FPT + 2 * D; ++i) {
             const int t = t0 + fr0 - D + i;
             const float vm = (t >= 0 && t < T) ? 1.f : 0.f;
             hv[i] = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(hb + i * CH), sc2, sh2) * vm;
           }
 #pragma unroll
-          for (int i = 0; i < F / 2; ++i) {
-            if (i % RS == 0) ring_load<PRE, LQ, RD>(w2, voff, rh, rl, i / RS, i / RS);  // res_out ring entry i/RS
+          for (int i = 0; i < FPT; ++i) {
+            if (i % RS == 0) ring_load<PRE, LQ, NWV, RD>(w2, voff, rh, rl, i / RS, i / RS);  // res_out ring entry i/RS
             const int tl = fr0 + i;
             const float vo = t0 + tl < T ? 1.f : 0.f;
             f32x2 y[2];
@@ -472,7 +507,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           default: rows(std::integral_constant<int, 4>{}); break;
         }
         float st[2] = {s0.x + s0.y, s1.x + s1.y};
-        block_sums<2>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
+        block_sums<2, NW>(st, sm.red, sm.dred);  // barrier inside: d complete in LDS
         T16P(4);
       }
       // ---- P2 words: GN2 partial sums (awaited inside the P3 round) ----
@@ -480,9 +515,9 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
       if (tid < 2) gputd(slot(g, e2) + GW_STAT + 2 * tid, tag2, sm.dred[tid], l2);
       // ================= res_out 512->256 (model/model.py:136,144) with reg2 folded =================
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      wave_gemm<NS2, LDD, PRE, LQ, RD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + L::W2 + (size_t)wave_s * NS2 * L::SB), voff, rh, rl,
-                                       lane);
+      for (int j = 0; j < TPW; ++j) acc[j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      wave_gemm<NS2, LDD, PRE, LQ, NWV, RD>(acc, sm.Ahi, sm.Alo, rsrc_of(wb + L::W2 + (size_t)wave_s * NS2 * L::SB), voff, rh,
+                                            rl, lane);
       T16P(5);
       // GN2 {mean, rstd} of the group (polled words in a wave's lanes, or in LDS)
       auto gn2_moments = [&](float& fmu, float& frs) {
@@ -513,7 +548,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         float fmu, frs;
         gn2_moments(fmu, frs);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           const int c = ch + 16 * j;
           const float ws = *P(sm, PB_WS2 + c), bias = *P(sm, PB_B2 + c), fcm = fmu * *P(sm, PB_FC2 + c);
 #pragma unroll
@@ -525,7 +560,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         {
           float csr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < TPW; ++j) {
             const int c = ch + 16 * j;
             const float ws = *P(sm, PB_WS2 + c);
             float rsum = 0.f;
@@ -539,7 +574,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
             if (lane < 16) gputf(slot(g, e3) + GW_ROW + c, tag3, rsum, l2);
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) csr[i] = row_total(csr[i]);  // ws-weighted sum over the wave's 64 channels
+          for (int i = 0; i < 4; ++i) csr[i] = row_total(csr[i]);  // ws-weighted sum over the wave's channels
           if ((lane & 15) == 15) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) sm.cs[f0 + i][wave_s] = csr[i];
@@ -567,10 +602,10 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           }
           float s = 0.f, vat = 0.f;
           unsigned vq = 0u;
-          for (int c0 = 0; c0 < G; c0 += PCH) {  // thread tid = channel tid: every member's row sum, member order
+          for (int c0 = 0; c0 < G; c0 += PCH) {  // thread tid < CH = channel tid: every member's row sum, member order
 #pragma unroll
             for (int mm = 0; mm < PCH; ++mm) {
-              pp[mm] = c0 + mm < G ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
+              pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
               tg[mm] = tag3;
             }
             pp[PCH] = (c0 == 0 && tid < 4 * G) ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr;  // GN2 words
@@ -596,8 +631,9 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           float fmu, frs;
           gn2_moments(fmu, frs);
           const float Tf = (float)T, sfc = *P(sm, PB_SFC2), sb = *P(sm, PB_SB2);
-          // a_f input: channel means of r over the utterance (GN2 fold applied to the sums); thread = channel
-          vec[tid + 4] = (frs * (*P(sm, PB_WS2 + tid) * s - Tf * fmu * *P(sm, PB_FC2 + tid)) + Tf * *P(sm, PB_B2 + tid)) / Tf;
+          // a_f input: channel means of r over the utterance (GN2 fold applied to the sums); thread tid < CH = channel
+          if (tid < CH)
+            vec[tid + 4] = (frs * (*P(sm, PB_WS2 + tid) * s - Tf * fmu * *P(sm, PB_FC2 + tid)) + Tf * *P(sm, PB_B2 + tid)) / Tf;
           if (tid < 4) { vec[tid] = 0.f; vec[CH + 4 + tid] = 0.f; yf[tid] = 0.f; yf[CH + 4 + tid] = 0.f; }
           if (mi >= 0) sm.mC[mi] = pat != nullptr ? (frs * (vat - fmu * sfc) + sb) / (float)CH : 0.f;
           if (tid >= 8 && tid < 8 + F) {
@@ -605,7 +641,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
             sm.mC[tl + 4] = (t0 + tl < T) ? (frs * (sm.csum[tl] - fmu * sfc) + sb) / (float)CH : 0.f;
           }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < TPW; ++j) {
             const int c = ch + 16 * j;
             const float ws = *P(sm, PB_WS2 + c), bias = *P(sm, PB_B2 + c), fcm = fmu * *P(sm, PB_FC2 + c);
 #pragma unroll
@@ -617,7 +653,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         const float* p = P(sm, PB_ATT);
         // a_f: mean over frames -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (channel axis);
         // a_t: mean over channels -> conv(d=1) -> conv(d=2) -> PReLU -> sigmoid (frame axis)
-        yf[tid + 4] = p[11] + p[8] * vec[tid + 3] + p[9] * vec[tid + 4] + p[10] * vec[tid + 5];
+        if (tid < CH) yf[tid + 4] = p[11] + p[8] * vec[tid + 3] + p[9] * vec[tid + 4] + p[10] * vec[tid + 5];
         if (tid < F + 8) {
           const int i = tid, t = t0 - 4 + i;
           float v = 0.f;
@@ -625,7 +661,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           sm.yt[i] = v;
         }
         __syncthreads();
-        {
+        if (tid < CH) {
           const float v = p[15] + p[12] * yf[tid + 2] + p[13] * yf[tid + 4] + p[14] * yf[tid + 6];
           sm.af[tid] = sigmoid_f(prelu_f(v, p[17]));
         }
@@ -638,10 +674,10 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
       }
       T16P(9);
       // ---- residual update (model/model.py:345-352): r' = r a_f a_t in place ----
-      if (DUMP && bi == 0) {  // parity probe: DepthConv1d output of block 0 (model/model.py:144), before the gates
+      if (DUMP && bi == kargs()->dump_blk) {  // parity probe: DepthConv1d output (model/model.py:144), before the gates
         if (float* dp = kargs()->dump) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < TPW; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i) dp[((size_t)(kargs()->B + u) * Tp + t0 + f0 + i) * CH + ch + 16 * j] = acc[j][i];
         }
@@ -651,23 +687,23 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) at4[i] = sm.at[f0 + i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           const float afm = sm.af[ch + 16 * j];
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[j][i] = acc[j][i] * (at4[i] * afm);
         }
       }
-      if (DUMP && bi == 0) {  // parity probe: TF_Attention output of block 0 (model/model.py:207)
+      if (DUMP && bi == kargs()->dump_blk) {  // parity probe: TF_Attention output (model/model.py:207)
         if (float* dp = kargs()->dump) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < TPW; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i) dp[((size_t)(2 * kargs()->B + u) * Tp + t0 + f0 + i) * CH + ch + 16 * j] = acc[j][i];
         }
       }
-      float kc[4][4];  // per channel j: GN_a scale, shift, GN_b scale, shift
+      float kc[TPW][4];  // per channel j: GN_a scale, shift, GN_b scale, shift
 #pragma unroll
-      for (int j = 0; j < 4; ++j) kc[j][0] = kc[j][1] = kc[j][2] = kc[j][3] = 0.f;
+      for (int j = 0; j < TPW; ++j) kc[j][0] = kc[j][1] = kc[j][2] = kc[j][3] = 0.f;
       if constexpr (LM == LD_RECURSIVE || LM == LD_RESIDUAL) {
         // moment record of u = o + r' (device_common.h recursive_affine): per channel five sums over the thread's
         // four frames, then the channel weights
@@ -675,7 +711,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
 #pragma unroll
         for (int k = 0; k < NMOM; ++k) mo[k] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
           const int c = ch + 16 * j;
           float so = 0.f, soo = 0.f, su = 0.f, suu = 0.f, sou = 0.f;
 #pragma unroll
@@ -697,13 +733,13 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
             mo[10] = fmaf(ga * ga, su, mo[10]);
           }
         }
-        block_sums<NMOM>(mo, sm.red, sm.dred);
+        block_sums<NMOM, NW>(mo, sm.red, sm.dred);
         T16P(10);
         // ---- P4 words: the moment record (11 doubles); consume every member's ----
         const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
         if (tid < NMOM) gputd(slot(g, e4) + GW_P4 + 2 * tid, tag4, sm.dred[tid], l2);
         {
-          constexpr int NPW = (2 * NMOM * GMAX + NT - 1) / NT;  // words per thread (3 at 32 members)
+          constexpr int NPW = (2 * NMOM * GMAX + NT - 1) / NT;  // words per thread
           const int nw = 2 * NMOM * G;
           const u64* pp[NPW];
           unsigned v[NPW];
@@ -736,7 +772,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           recursive_moments_f(ms, reinterpret_cast<const double*>(P(sm, PB_WSUM)), 1e-5f, 1e-5f, a.inv_ch, (double)T, mua,
                               rsa, mub, rsb);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < TPW; ++j) {
             const int c = ch + 16 * j;
             kc[j][0] = rsa * *P(sm, PB_LNAG + c); kc[j][1] = *P(sm, PB_LNAB + c) - kc[j][0] * mua;
             kc[j][2] = rsb * *P(sm, PB_LNBG + c); kc[j][3] = *P(sm, PB_LNBB + c) - kc[j][2] * mub;
@@ -745,7 +781,7 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
           float mu, rs;
           gn_moments_f(ms[2], ms[3], a.inv_ch, 1e-5f, mu, rs);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < TPW; ++j) {
             const int c = ch + 16 * j;
             kc[j][0] = rs * *P(sm, PB_LNAG + c); kc[j][1] = *P(sm, PB_LNAB + c) - kc[j][0] * mu;
           }
@@ -758,11 +794,11 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
         const __amdgpu_buffer_rsrc_t w1n = rsrc_of(wn + L::W1 + (size_t)wave_s * NS1 * L::SB);
         const float sxn = *P(sm, PB_SXN);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
 #pragma unroll
           for (int i = 0; i < 4; i += 2) {
-            const int r = 2 * j + i / 2;  // row-pair index 0..7
-            if (r % RS == 0) ring_load<PRE, LQ, RD>(w1n, voff, rh, rl, r / RS, r / RS);
+            const int r = 2 * j + i / 2;  // row-pair index 0..2 TPW - 1
+            if (r % RX == 0) ring_load<PRE, LQ, NWV, RD>(w1n, voff, rh, rl, r / RX, r / RX);
             const f32x2 x = resid_apply2<LM>(f32x2{o[4 * j + i], o[4 * j + i + 1]}, f32x2{acc[j][i], acc[j][i + 1]}, kc[j]);
             const f32x2 ov = x * f32x2{fm(i), fm(i + 1)};
             o[4 * j + i] = ov.x; o[4 * j + i + 1] = ov.y;
@@ -776,11 +812,11 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
     // ---- TCN output x' (head input) and the statistics of PReLU(x') for TCN.output.1 ----
     {
       const int tidt = fresh_tid(wave_s);
-      const int f0 = 4 * ((tidt & 63) >> 4), ch = 64 * wave_s + (tidt & 15);
+      const int f0 = 4 * ((tidt & 63) >> 4), ch = CPW * wave_s + (tidt & 15);
       float st[2] = {0.f, 0.f};
       float* Xu = a.Xfin + ((size_t)u * Tp + t0) * CH;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int t = t0 + f0 + i;
@@ -793,12 +829,12 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
       // k_head reads 32-frame slices: an odd group's last member also zeroes the 16 rows past its own (t >= T)
       if ((G & 1) && g == G - 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (t0 + F + f0 + i < Tp) st_out(Xu + (F + f0 + i) * CH + ch + 16 * j, 0.f);
       }
-      block_sums<2>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
+      block_sums<2, NW>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
       __syncthreads();
     }
   }
@@ -809,78 +845,100 @@ __global__ __launch_bounds__(NT, 2) void k_tcn16(TcnArgs a) {
   }
 }
 
-template <int PRE, int LQ>
+// diagnostics (SEPVAD_TCN16_DYNLDS = bytes): unused dynamic LDS per workgroup, so fewer workgroups fit a CU (the
+// capacity follows: hipOccupancy sees the same size)
+inline size_t dyn_lds() {
+  const char* v = getenv("SEPVAD_TCN16_DYNLDS");
+  return v ? (size_t)atol(v) : 0;
+}
+
+template <int PRE, int LQ, int NWV>
 hipError_t launch_pre(const TcnArgs& a, int grid, hipStream_t s) {
+  const dim3 blk(64 * NWV);
   if (a.probe != nullptr && a.ln_mode == LD_RECURSIVE) {  // phase-stamp instantiation (SEPVAD_TCN_PROBE)
-    hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, false, LQ, true>), dim3(grid), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, NWV, false, LQ, true>), dim3(grid), blk, dyn_lds(), s, a);
     return hipGetLastError();
   }
   if (a.dump != nullptr) {  // parity-probe instantiation
     switch (a.ln_mode) {
-      case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, true, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
-      case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn16<LD_RESIDUAL, PRE, true, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
-      case LD_ADD: hipLaunchKernelGGL((k_tcn16<LD_ADD, PRE, true, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
+      case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, NWV, true, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
+      case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn16<LD_RESIDUAL, PRE, NWV, true, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
+      case LD_ADD: hipLaunchKernelGGL((k_tcn16<LD_ADD, PRE, NWV, true, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (a.ln_mode) {
-    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, false, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
-    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn16<LD_RESIDUAL, PRE, false, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
-    case LD_ADD: hipLaunchKernelGGL((k_tcn16<LD_ADD, PRE, false, LQ>), dim3(grid), dim3(NT), 0, s, a); break;
+    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn16<LD_RECURSIVE, PRE, NWV, false, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
+    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn16<LD_RESIDUAL, PRE, NWV, false, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
+    case LD_ADD: hipLaunchKernelGGL((k_tcn16<LD_ADD, PRE, NWV, false, LQ>), dim3(grid), blk, dyn_lds(), s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-template <int PRE, int LQ>
+template <int PRE, int LQ, int NWV>
 int blocks_pre(int ln_mode) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
+  const int nt = 64 * NWV;
   switch (ln_mode) {
-    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_RECURSIVE, PRE, false, LQ>, NT, 0); break;
-    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_RESIDUAL, PRE, false, LQ>, NT, 0); break;
-    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_ADD, PRE, false, LQ>, NT, 0); break;
+    case LD_RECURSIVE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_RECURSIVE, PRE, NWV, false, LQ>, nt, dyn_lds()); break;
+    case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_RESIDUAL, PRE, NWV, false, LQ>, nt, dyn_lds()); break;
+    case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn16<LD_ADD, PRE, NWV, false, LQ>, nt, dyn_lds()); break;
   }
   return e == hipSuccess ? nb : 0;
+}
+
+template <int NWV>
+hipError_t launch_w(const TcnArgs& a, int grid, hipStream_t s) {
+  switch (a.prec) {
+    case PREC_F16X3:
+      switch (a.lo8) {
+        case 0: return launch_pre<PREC_F16X3, 0, NWV>(a, grid, s);
+        case 1: return launch_pre<PREC_F16X3, 1, NWV>(a, grid, s);
+        case 2: return launch_pre<PREC_F16X3, 2, NWV>(a, grid, s);
+      }
+      return hipErrorInvalidValue;
+    case PREC_F16: return launch_pre<PREC_F16, 0, NWV>(a, grid, s);
+    case PREC_BF16: return launch_pre<PREC_BF16, 0, NWV>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int NWV>
+int blocks_w(int ln_mode, int prec, int lo) {
+  switch (prec) {
+    case PREC_F16X3:
+      return lo == 1 ? blocks_pre<PREC_F16X3, 1, NWV>(ln_mode)
+                     : (lo == 2 ? blocks_pre<PREC_F16X3, 2, NWV>(ln_mode) : blocks_pre<PREC_F16X3, 0, NWV>(ln_mode));
+    case PREC_F16: return blocks_pre<PREC_F16, 0, NWV>(ln_mode);
+    case PREC_BF16: return blocks_pre<PREC_BF16, 0, NWV>(ln_mode);
+  }
+  return 0;
 }
 
 }  // namespace t16
 
 size_t tcn16_block_bytes(int prec, int lo) {
+  // the same for 4 and 8 waves (every wave's chunks together are the block's weights)
   switch (prec) {
-    case PREC_F16X3: return lo == 0 ? t16::Lay<PREC_F16X3, 0>::BLOCK : t16::Lay<PREC_F16X3, 2>::BLOCK;
-    case PREC_F16: case PREC_BF16: return t16::Lay<PREC_F16, 0>::BLOCK;
+    case PREC_F16X3: return lo == 0 ? t16::Lay<PREC_F16X3, 0, 8>::BLOCK : t16::Lay<PREC_F16X3, 2, 8>::BLOCK;
+    case PREC_F16: case PREC_BF16: return t16::Lay<PREC_F16, 0, 8>::BLOCK;
   }
   return 0;
 }
 
-hipError_t launch_tcn16(const TcnArgs& a, int grid, hipStream_t s) {
+hipError_t launch_tcn16(const TcnArgs& a, int grid, int nwaves, hipStream_t s) {
   if (a.G < 1 || a.G > FG16_MAX || a.G * FR16 < a.T || a.G * FR16 > a.Tp || grid < a.G || grid % a.G)
     return hipErrorInvalidValue;
-  switch (a.prec) {
-    case PREC_F16X3:
-      switch (a.lo8) {
-        case 0: return t16::launch_pre<PREC_F16X3, 0>(a, grid, s);
-        case 1: return t16::launch_pre<PREC_F16X3, 1>(a, grid, s);
-        case 2: return t16::launch_pre<PREC_F16X3, 2>(a, grid, s);
-      }
-      return hipErrorInvalidValue;
-    case PREC_F16: return t16::launch_pre<PREC_F16, 0>(a, grid, s);
-    case PREC_BF16: return t16::launch_pre<PREC_BF16, 0>(a, grid, s);
-  }
+  if (nwaves == 4) return t16::launch_w<4>(a, grid, s);
+  if (nwaves == 8) return t16::launch_w<8>(a, grid, s);
   return hipErrorInvalidValue;
 }
 
-int tcn16_blocks_per_cu(int ln_mode, int prec, int lo) {
-  switch (prec) {
-    case PREC_F16X3:
-      return lo == 1 ? t16::blocks_pre<PREC_F16X3, 1>(ln_mode)
-                     : (lo == 2 ? t16::blocks_pre<PREC_F16X3, 2>(ln_mode) : t16::blocks_pre<PREC_F16X3, 0>(ln_mode));
-    case PREC_F16: return t16::blocks_pre<PREC_F16, 0>(ln_mode);
-    case PREC_BF16: return t16::blocks_pre<PREC_BF16, 0>(ln_mode);
-  }
-  return 0;
+int tcn16_blocks_per_cu(int ln_mode, int prec, int lo, int nwaves) {
+  return nwaves == 4 ? t16::blocks_w<4>(ln_mode, prec, lo) : (nwaves == 8 ? t16::blocks_w<8>(ln_mode, prec, lo) : 0);
 }
 
 }  // namespace sepvad

@@ -333,14 +333,15 @@ struct TcnArgs {
   float* dump;           // parity probe (sepvad_set_tcn_dump), nullable: [3][B][Tp][CH] = TCN.LN output x'_0,
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
   unsigned dbg_delay;    // diagnostics (SEPVAD_TCN_DELAY): member 0 of each group sleeps before its polls (0: off)
+  int dump_blk;          // parity probe: the block whose input (dump slot 0 when > 0), r and r a_f a_t are dumped
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
 // The same TCN on 16-frame members, two 256-thread workgroups per CU (fused16.hip k_tcn16); TcnArgs.G counts
 // 16-frame members, wfrag is the k_tcn16 blob (tcn16_block_bytes per block), rec_head [B][G][2]
 constexpr int FR16 = 16;
 constexpr int FG16_MAX = 32;    // members per group (T <= 512); longer utterances run k_tcn
-hipError_t launch_tcn16(const TcnArgs& a, int grid, hipStream_t s);
-int tcn16_blocks_per_cu(int ln_mode, int prec, int lo);
+hipError_t launch_tcn16(const TcnArgs& a, int grid, int nwaves, hipStream_t s);  // nwaves: 4 or 8 per workgroup
+int tcn16_blocks_per_cu(int ln_mode, int prec, int lo, int nwaves);
 size_t tcn16_block_bytes(int prec, int lo);
 // Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
 // for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).

@@ -41,3 +41,23 @@ def state_dicts():
     for c in CONFIGS:
         out[c] = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(config_of(c), 1234).items()}
     return out
+
+
+def check_vad_labels(vad, v_ref, band=1e-4, flips_per=1e-4, where=""):
+    """VAD labels (p >= 0.5, reference model/model.py:449) vs the reference probabilities: bit-exact wherever the
+    reference is farther than `band` from the threshold; inside the band (where fp32 rounding of either side can move
+    a probability across 0.5) the labels are counted, not skipped: at most one flip per 1/flips_per labels (and at
+    least one allowed). Returns (labels, labels in the band, flips in the band); printed for the test log."""
+    vad = np.asarray(vad)
+    v_ref = np.asarray(v_ref)
+    lab, lref = vad >= 0.5, v_ref >= 0.5
+    near = np.abs(v_ref - 0.5) <= band
+    far_flips = int((lab != lref)[~near].sum())
+    near_flips = int((lab != lref)[near].sum())
+    n, nb = lab.size, int(near.sum())
+    allowed = max(1, int(n * flips_per))
+    msg = f"{where} VAD labels: {n}, within {band:g} of 0.5: {nb}, flips there: {near_flips} (allowed {allowed})"
+    print(msg)
+    assert far_flips == 0, f"{msg}; flips outside the band: {far_flips}"
+    assert near_flips <= allowed, msg
+    return n, nb, near_flips

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import config_of, load_golden
+from conftest import check_vad_labels, config_of, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -197,9 +197,7 @@ def test_scaled_weights_keep_fp32_accuracy(wscale, state_dicts):
     e32 = (s32 - s64).abs().max().item()
     ehip = (s.cpu().double() - s64).abs().max().item()
     assert ehip <= max(SEP_TOL, 3.0 * e32), (ehip, e32)
-    vr = v64.numpy()
-    safe = np.abs(vr - 0.5) > 1e-3
-    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    check_vad_labels(v.cpu().numpy(), v64.numpy(), band=1e-3, where=f"weights x{wscale:g}")
 
 
 @pytest.mark.parametrize("xscale", [1e-3, 1e3])
@@ -211,9 +209,7 @@ def test_scaled_inputs(xscale, net, state_dicts):
         s, v, _ = net(x.to(DEV))
     s_ref, v_ref, _ = OracleModel(config_of("with_vad"), state_dicts["with_vad"], torch.float32)(x)
     assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL * max(1.0, xscale)
-    vr = v_ref.numpy()
-    safe = np.abs(vr - 0.5) > 1e-4
-    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    check_vad_labels(v.cpu().numpy(), v_ref.numpy())
 
 
 def test_side_attributes_materialised_on_read(net):
@@ -263,9 +259,7 @@ def test_shortest_input_and_too_short_input(net, state_dicts):
     s_ref, v_ref, _ = om(x)
     assert s.shape == s_ref.shape and v.shape == v_ref.shape
     assert np.abs(s.cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
-    vr = v_ref.numpy()
-    safe = np.abs(vr - 0.5) > 1e-4
-    assert np.array_equal((v.cpu().numpy() >= 0.5)[safe], (vr >= 0.5)[safe])
+    check_vad_labels(v.cpu().numpy(), v_ref.numpy())
     x = x[:, :256].contiguous()
     with pytest.raises(RuntimeError):
         om(x)
