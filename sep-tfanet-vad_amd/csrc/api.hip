@@ -51,10 +51,6 @@ struct PackedW {
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
   size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
   size_t fi8 = 0;           // ... the same as int8 steps of 2^-WQ_LO_SHIFT, biased by 128
-  // k_tcn16 (fused16.hip, v_mfma_f32_16x16x32) B-fragment order: fp16 planes [mpad/16 tiles][cin/32 steps][64][8 halves],
-  // lane l -> row 16 nt + (l & 15), k = 32 s + 8 (l >> 4) + j; byte planes [mpad/32 tile pairs][cin/32][64][16 bytes:
-  // 8 of tile 2 pp, then 8 of tile 2 pp + 1]
-  size_t ghi = 0, glo = 0, gbf = 0, gf8 = 0, gi8 = 0;
 };
 
 struct BlockOff {
@@ -165,11 +161,6 @@ struct sepvad_model {
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
-  // k_tcn16 (fused16.hip: 16-frame members, two workgroups per CU) for T <= 16 * FG16_MAX; opt-in (SEPVAD_TCN16=1)
-  bool tcn16 = false;
-  int t16_waves = 8;            // waves per k_tcn16 workgroup (SEPVAD_TCN16_WAVES=4|8; the blob layout follows)
-  char* t16w[5] = {};           // [nblk][tcn16_block_bytes] blobs: [0..2] F16X3 with the fp16 / e4m3 / int8 lo plane, [3] F16, [4] BF16
-  int tcn16_cap[5] = {};        // co-resident k_tcn16 workgroups per variant
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
   float* tdump = nullptr;       // parity probe buffer of the fused TCN (sepvad_set_tcn_dump), caller-owned
@@ -351,36 +342,6 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
       p.fi8 = pk.addh(f8h);
     }
   }
-  if (mpad % 32 == 0 && cin % 32 == 0) {
-    const size_t n = (size_t)mpad * cin;
-    std::vector<__half> gh(n), gl(n), gb(n);
-    std::vector<uint8_t> g8(n), gi(n);
-    size_t q = 0;
-    for (int nt = 0; nt < mpad / 16; ++nt)
-      for (int st = 0; st < cin / 32; ++st)
-        for (int l = 0; l < 64; ++l)
-          for (int j = 0; j < 8; ++j, ++q) {
-            const size_t src = (size_t)(16 * nt + (l & 15)) * cin + 32 * st + 8 * (l >> 4) + j;
-            gh[q] = hi[src]; gl[q] = lo[src]; gb[q] = bf[src];
-          }
-    size_t b = 0;
-    for (int pp = 0; pp < mpad / 32; ++pp)
-      for (int st = 0; st < cin / 32; ++st)
-        for (int l = 0; l < 64; ++l)
-          for (int h = 0; h < 2; ++h)
-            for (int j = 0; j < 8; ++j, ++b) {
-              const size_t src = (size_t)(32 * pp + 16 * h + (l & 15)) * cin + 32 * st + 8 * (l >> 4) + j;
-              g8[b] = e4m3_rn(lo32[src] * (float)(1 << WQ_LO_SHIFT));
-              const double qv = std::nearbyint(std::ldexp((double)lo32[src], WQ_LO_SHIFT));
-              gi[b] = (uint8_t)(std::max(-128.0, std::min(127.0, qv)) + 128.0);
-            }
-    p.ghi = pk.addh(gh); p.glo = pk.addh(gl); p.gbf = pk.addh(gb);
-    std::vector<__half> tmp(n / 2);
-    std::memcpy(tmp.data(), g8.data(), n);
-    p.gf8 = pk.addh(tmp);
-    std::memcpy(tmp.data(), gi.data(), n);
-    p.gi8 = pk.addh(tmp);
-  }
   return p;
 }
 
@@ -516,42 +477,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q[q]);
   }
-  for (int v = 0; v < 5; ++v) {
-    const int p = v < 3 ? PREC_F16X3 : (v == 3 ? PREC_F16 : PREC_BF16);
-    h->tcn16_cap[v] = ncu * tcn16_blocks_per_cu(ln, p, v < 3 ? v : 0, h->t16_waves);
-    h->tcn_cap = std::max(h->tcn_cap, h->tcn16_cap[v]);  // the hand-off words serve either kernel
-  }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
-  // k_tcn16 blobs: per block and GEMM, per (wave, K step of 32) one chunk: the wave's 4 hi tiles, then its lo plane
-  // (fp16: 4 tiles; e4m3 / int8: 2 tile pairs), all in v_mfma_f32_16x16x32 B-fragment order (pack_pointwise g*)
-  for (int v = 0; v < 5; ++v) {
-    const int p = v < 3 ? PREC_F16X3 : (v == 3 ? PREC_F16 : PREC_BF16), lo = v < 3 ? v : 0;
-    const size_t blk = tcn16_block_bytes(p, lo);
-    std::vector<char> bl(blk * h->nblk);
-    for (int i = 0; i < h->nblk; ++i) {
-      char* d = bl.data() + blk * i;
-      for (const PackedW* pw : {&h->blk[i].w1, &h->blk[i].w2}) {
-        const int ns = pw == &h->blk[i].w1 ? CH / 32 : HID / 32;
-        const __half* hi = pk.hblob.data() + (v == 4 ? pw->gbf : pw->ghi);
-        const __half* lp = pk.hblob.data() + (lo == 0 ? pw->glo : (lo == 1 ? pw->gf8 : pw->gi8));
-        const int nw = h->t16_waves, tpw = 16 / nw;  // waves, 16-channel tiles per wave
-        for (int w = 0; w < nw; ++w)
-          for (int st = 0; st < ns; ++st) {
-            for (int j = 0; j < tpw; ++j, d += 1024) std::memcpy(d, hi + ((size_t)(tpw * w + j) * ns + st) * 512, 1024);
-            if (v < 3) {
-              if (lo == 0)
-                for (int j = 0; j < tpw; ++j, d += 1024) std::memcpy(d, lp + ((size_t)(tpw * w + j) * ns + st) * 512, 1024);
-              else
-                for (int q = 0; q < tpw / 2; ++q, d += 1024)
-                  std::memcpy(d, lp + ((size_t)(tpw / 2 * w + q) * ns + st) * 512, 1024);
-            }
-          }
-      }
-      if (d != bl.data() + blk * (i + 1)) { g_err = "k_tcn16 blob layout"; return SEPVAD_E_ARG; }
-    }
-    HIPCHK(hipMalloc(&h->t16w[v], bl.size()));
-    HIPCHK(hipMemcpy(h->t16w[v], bl.data(), bl.size(), hipMemcpyHostToDevice));
-  }
   std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
@@ -978,8 +904,6 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     return nullptr;
   }
   if (const char* fz = getenv("SEPVAD_FUSED")) h->fused = atoi(fz) != 0;
-  if (const char* t16 = getenv("SEPVAD_TCN16")) h->tcn16 = atoi(t16) != 0;
-  if (const char* t16w = getenv("SEPVAD_TCN16_WAVES")) h->t16_waves = atoi(t16w) == 4 ? 4 : 8;
   if (const char* wl = getenv("SEPVAD_WLO")) {  // "i8" (default) | "f16" | "e4m3"; anything else is an error
     if (std::strcmp(wl, "e4m3") == 0) h->lo8 = 1;
     else if (std::strcmp(wl, "f16") == 0) h->lo8 = 0;
@@ -1058,16 +982,9 @@ int tcn_cap_of(const sepvad_model* h) {
   return h->prec == PREC_F16X3 && h->lo8 ? h->tcn_cap_q[h->lo8] : h->tcn_cap_p[h->prec];
 }
 
-// k_tcn16 (fused16.hip) variant of the current precision / lo plane, and whether it runs at T
-int tcn16_variant(const sepvad_model* h) { return h->prec == PREC_F16X3 ? h->lo8 : (h->prec == PREC_F16 ? 3 : 4); }
-bool use_tcn16(const sepvad_model* h, int T) {
-  const int G = (T + FR16 - 1) / FR16;
-  return h->fused && h->tcn16 && h->prec != PREC_F32 && G <= FG16_MAX && h->tcn16_cap[tcn16_variant(h)] >= G;
-}
-
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return use_tcn16(h, T) || (h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G);
+  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G;
 }
 
 int env_int(const char* name, int dflt) {
@@ -1184,9 +1101,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
     // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
-    // k_tcn16 (16-frame members, two workgroups per CU) when the utterance fits its groups, else k_tcn
-    const bool t16 = use_tcn16(h, T);
-    const int Gt = t16 ? (T + FR16 - 1) / FR16 : G;  // members per utterance of the kernel that runs
+    const int Gt = G;  // workgroups per utterance
     TcnArgs ta{};
     ta.T = T; ta.Tp = Tp; ta.G = Gt; ta.nblk = h->nblk; ta.layer = c.layer;
     if (const int nb = env_int("SEPVAD_TCN_NBLK", 0); nb > 0 && nb < h->nblk) ta.nblk = nb;  // diagnostics: truncated stack
@@ -1195,21 +1110,18 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.prec = h->prec;
     ta.lo8 = h->prec == PREC_F16X3 ? h->lo8 : 0;
     ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq[ta.lo8] : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
-    if (t16) ta.wfrag = (const __half*)h->t16w[tcn16_variant(h)];
     ta.prm = h->tprm;
     ta.inv_ch = 1.0 / ((double)CH * T);
     ta.inv_hid = 1.0 / ((double)HID * T);
     ta.alpha_h = h->out_a;
     ta.gran = cx->tgran; ta.err = cx->terr; ta.herr = cx->herr_dev;
     ta.xmode = env_int("SEPVAD_TCN_XMODE", 0);
-    auto launch_t = [&](const TcnArgs& t, int grid) {
-      return t16 ? launch_tcn16(t, grid, h->t16_waves, s) : launch_tcn(t, grid, s);
-    };
+    auto launch_t = [&](const TcnArgs& t, int grid) { return launch_tcn(t, grid, s); };
     ta.spin_limit = (unsigned)env_int("SEPVAD_TCN_SPIN_LIMIT", 1 << 20);
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     ta.dbg_delay = (unsigned)std::max(0, env_int("SEPVAD_TCN_DELAY", 0));
     ta.dump_blk = std::max(0, std::min(h->nblk - 1, env_int("SEPVAD_TCN_DUMP_BLOCK", 0)));
-    int ngroups = std::min(B, (t16 ? h->tcn16_cap[tcn16_variant(h)] : tcn_cap_of(h)) / Gt);
+    int ngroups = std::min(B, tcn_cap_of(h) / Gt);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
     // counted as 4 (headroom)
@@ -1260,8 +1172,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         HIPCHK(hipMemsetAsync(ta.clk, 0, 8 * sizeof(unsigned long long), s));
       }
       if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
-        fprintf(stderr, "sepvad: %s grid=%d G=%d groups=%d B=%d capacity=%d\n", t16 ? "k_tcn16" : "k_tcn", ngl * Gt, Gt,
-                ngl, Bl, t16 ? h->tcn16_cap[tcn16_variant(h)] : tcn_cap_of(h));
+        fprintf(stderr, "sepvad: k_tcn grid=%d G=%d groups=%d B=%d capacity=%d\n", ngl * Gt, Gt, ngl, Bl, tcn_cap_of(h));
       if (ev()) return SEPVAD_E_HIP;
       HIPCHK(launch_t(ta, ngl * Gt));
       if (ev()) return SEPVAD_E_HIP;
@@ -1917,8 +1828,6 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->twf16) (void)hipFree(h->twf16);
   if (h->twbf) (void)hipFree(h->twbf);
   if (h->tprm) (void)hipFree(h->tprm);
-  for (char* q : h->t16w)
-    if (q) (void)hipFree(q);
   if (h->tprobe) (void)hipFree(h->tprobe);
   if (h->tclk) (void)hipFree(h->tclk);
   if (h->kprobe) (void)hipFree(h->kprobe);

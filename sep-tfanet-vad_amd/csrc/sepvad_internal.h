@@ -336,20 +336,13 @@ struct TcnArgs {
   int dump_blk;          // parity probe: the block whose input (dump slot 0 when > 0), r and r a_f a_t are dumped
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
-// The same TCN on 16-frame members, two 256-thread workgroups per CU (fused16.hip k_tcn16); TcnArgs.G counts
-// 16-frame members, wfrag is the k_tcn16 blob (tcn16_block_bytes per block), rec_head [B][G][2]
-constexpr int FR16 = 16;
-constexpr int FG16_MAX = 32;    // members per group (T <= 512); longer utterances run k_tcn
-hipError_t launch_tcn16(const TcnArgs& a, int grid, int nwaves, hipStream_t s);  // nwaves: 4 or 8 per workgroup
-int tcn16_blocks_per_cu(int ln_mode, int prec, int lo, int nwaves);
-size_t tcn16_block_bytes(int prec, int lo);
 // Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
 // for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
 struct HeadArgs {
   int B, T, Tp, G, prec;
   const float* Xfin;     // [B][Tp][CH] TCN output x'
-  const double* rec;     // [B][Grec][2] (sum, sumsq) of PReLU(x') per k_tcn / k_tcn16 member
-  int Grec;              // records per utterance (k_tcn: G; k_tcn16: its 16-frame members)
+  const double* rec;     // [B][Grec][2] (sum, sumsq) of PReLU(x') per k_tcn member
+  int Grec;              // records per utterance (k_tcn's workgroups per utterance)
   const float* g; const float* be;  // TCN.output.1 affine
   float alpha;           // TCN.output.0 PReLU
   float sx;              // range scale of the A operand (undone by wscale)

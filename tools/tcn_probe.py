@@ -77,34 +77,3 @@ def main(path):
 if __name__ == "__main__":
     main(sys.argv[1])
 
-
-def pairs(path):
-    """k_tcn16 probes: HW_ID / XCC_ID of every workgroup (last block's slots 13 / 14): workgroups per CU and, for CUs
-    hosting two, the offset between their block-start phases (fraction of a block)."""
-    raw = np.fromfile(path, dtype=np.int64)
-    grid, nblk, G, T = (int(v) for v in raw[:4])
-    full = raw[4:4 + grid * nblk * 16].reshape(grid, nblk, 16)
-    hw, xcc = full[:, -1, 13], full[:, -1, 14]
-    cu = (hw >> 8) & 0xF
-    sh = (hw >> 12) & 0x1
-    se = (hw >> 13) & 0x7
-    key = xcc * 1000 + se * 100 + sh * 20 + cu
-    u, cnt = np.unique(key, return_counts=True)
-    print(f"distinct CUs {len(u)}; workgroups per CU: " + ", ".join(f"{c}x{n}" for c, n in zip(*np.unique(cnt, return_counts=True))))
-    st = full[:, :, 0].astype(np.float64) / 100.0
-    blk = np.median(st[:, -1] - st[:, 1]) / max(1, nblk - 2)
-    offs = []
-    for k in u[cnt == 2]:
-        a, b = np.nonzero(key == k)[0]
-        offs.append(((st[a, 2:] - st[b, 2:]) / blk) % 1.0)
-    if offs:
-        o = np.array(offs)
-        o = np.minimum(o, 1 - o)
-        print(f"paired workgroups: phase offset (fraction of a block, 0 = in phase, 0.5 = anti-phase): median "
-              f"{np.median(o):.2f}, p10 {np.percentile(o, 10):.2f}, p90 {np.percentile(o, 90):.2f}")
-        same_grp = sum(1 for k in u[cnt == 2] if len({int(i) // G for i in np.nonzero(key == k)[0]}) == 1)
-        print(f"  pairs on one CU from blockIdx/G-adjacent members: {same_grp} of {len(offs)}")
-
-
-if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "pairs":
-    pairs(sys.argv[1])
