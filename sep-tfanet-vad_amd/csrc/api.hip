@@ -992,6 +992,25 @@ int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
+// Progress of concurrent fused launches (include/sepvad.h: concurrent forwards on different streams are allowed).
+// A k_tcn group waits for all of its G members, and the grid is dealt in order, so a launch progresses as long as
+// 8 G of its workgroups are resident (fused.hip header). Two launches that each need more than half the chip for
+// that can each hold part of the CUs and wait on each other until the give-up bound. Such "big" launches (long
+// utterances) are therefore ordered across streams, process-wide per device: each waits on the previous one's
+// completion event (stream-ordered, no host sync). Launches of small groups need no ordering: any resident prefix
+// of 8 G workgroups completes them, beside a big launch too, and they free their CUs.
+bool tcn_big(const sepvad_model* h, int G) { return 8 * G > tcn_cap_of(h) / 2; }
+int tcn_order_big(int device, hipStream_t s, bool after) {
+  static std::mutex mu;
+  static std::unordered_map<int, hipEvent_t> last;  // device -> the last big launch's completion
+  std::lock_guard<std::mutex> lk(mu);
+  hipEvent_t& e = last[device];
+  if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (after) HIPCHK(hipEventRecord(e, s));
+  else HIPCHK(hipStreamWaitEvent(s, e, 0));
+  return SEPVAD_OK;
+}
+
 // Per-forward timing state (sepvad_set_timing): HIP events around the GEMM launches of chunk 0.
 struct TimingRec {
   std::vector<int> gemm_ev, g2_ev;
@@ -1173,9 +1192,12 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       }
       if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
         fprintf(stderr, "sepvad: k_tcn grid=%d G=%d groups=%d B=%d capacity=%d\n", ngl * Gt, Gt, ngl, Bl, tcn_cap_of(h));
+      const bool big = tcn_big(h, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
+      if (big && tcn_order_big(h->device, s, false)) return SEPVAD_E_HIP;
       if (ev()) return SEPVAD_E_HIP;
       HIPCHK(launch_t(ta, ngl * Gt));
       if (ev()) return SEPVAD_E_HIP;
+      if (big && tcn_order_big(h->device, s, true)) return SEPVAD_E_HIP;
       if (tr) {
         tr->gemm_ev.push_back((int)h->ev.size() - 2);
         tr->g2_ev.push_back((int)h->ev.size() - 2);

@@ -335,3 +335,30 @@ def test_salt_wrap_restarts_giveup_words(net):
     finally:
         del os.environ["SEPVAD_TCN_SALT_MAX"]
         h.release_stream(s.cuda_stream)
+
+
+def test_concurrent_long_forwards_make_progress(net):
+    """Three streams of one handle forwarding B=2 x 60 s files at once (T = 3751: groups of 118 workgroups, more than
+    half the chip each): the big persistent launches are ordered across streams (api.hip tcn_order_big), so none
+    waits on a group that can never become resident. No give-up, every output equal to the serial run, fused."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    xs = [torch.from_numpy(synth.make_batch(2, 960000, 600 + k)[0]).to(DEV) for k in range(3)]
+    ref = []
+    for x in xs:
+        r = h.forward(x)
+        ref.append({k: r[k].clone() for k in ("sep", "vad", "est")})
+    assert h.fused_status()
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in xs]
+    outs = []
+    for x, st in zip(xs, streams):
+        with torch.cuda.stream(st):
+            outs.append(h.forward(x))
+    torch.cuda.synchronize()
+    assert h.fused_status()
+    for o, r in zip(outs, ref):
+        for k in ("sep", "vad", "est"):
+            assert torch.equal(o[k], r[k]), k
+    for st in streams:
+        h.release_stream(st.cuda_stream)
