@@ -337,6 +337,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (tid < FR) sm.at[tid] = 1.f;
   }
   bool l2 = false;
+  // groups above FG_TREE members reduce the P3 row sums and the P4 moment records in two levels: member g's words go
+  // to leader g % 8 (the members of one leader share blockIdx % 8, one XCD under round-robin dispatch: speed only),
+  // every member then polls the 8 leaders' partial sums -- 3 hand-off round trips instead of G / 8 (P3) and a 176-
+  // word poll instead of 22 G words (P4). sl2: the member and its leader share an XCD (checked at epoch 1)
+  const bool tree = G > FG_TREE;
+  bool sl2 = false;
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
@@ -394,9 +400,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       gpoll<1>(p, a.tag0 + 1, v, a);
       if (tid < G) sm.gw[tid] = v[0];
       __syncthreads();
-      bool same = a.xmode == 0;
-      for (int mm = 0; mm < G; ++mm) same = same && sm.gw[mm] == sm.gw[0];
+      bool same = a.xmode == 0, sub = a.xmode == 0;
+      for (int mm = 0; mm < G; ++mm) {
+        same = same && sm.gw[mm] == sm.gw[0];
+        sub = sub && (mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8]);
+      }
       l2 = same;
+      sl2 = sub;
       if (TP_ON && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
     }
     __syncthreads();  // LN record sums (sm.dred) complete
@@ -768,7 +778,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             for (int r = 0; r < 16; ++r) sm.cs[trow(r)][wave] = csr[r];
           }
           rsum += __shfl_xor(rsum, 32);
-          if (hl == 0) gputf(slot(g, e3) + GW_ROW + m, tag3, rsum, l2);
+          if (hl == 0) gputf(slot(g, e3) + GW_ROW + m, tag3, rsum, tree ? sl2 : l2);
         }
         __syncthreads();  // cs complete; also: every wave is done reading d from LDS
       TPROBE(6);
@@ -797,10 +807,30 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int kq = tid - (NTHR - 128);
           float s = 0.f, vat = 0.f;
           unsigned vq[4] = {0u, 0u, 0u, 0u};
-          for (int c0 = 0; c0 < G; c0 += FG_CHUNK) {
+          if (tree) {
+            // level 1 (leaders g < 8): the row sums of members g, g + 8, ..., member order, published write-through
+            if (g < 8) {
+              float ss = 0.f;
+              for (int c0 = g; c0 < G; c0 += 8 * FG_CHUNK) {
+#pragma unroll
+                for (int mm = 0; mm < FG_CHUNK; ++mm) {
+                  pp[mm] = (tid < CH && c0 + 8 * mm < G) ? slot(c0 + 8 * mm, e3) + GW_ROW + tid : nullptr;
+                  tg[mm] = tag3;
+                }
+                gpollt<FG_CHUNK>(pp, tg, v, a);
+#pragma unroll
+                for (int mm = 0; mm < FG_CHUNK; ++mm)
+                  if (c0 + 8 * mm < G) ss += __builtin_bit_cast(float, v[mm]);
+              }
+              if (tid < CH) gputf(slot(g, e3) + GW_SUB3 + tid, tag3, ss, false);
+            }
+          }
+          static_assert(FG_CHUNK == 8, "level 2 of the P3 tree polls the 8 leaders in one pass");
+          for (int c0 = 0; c0 < (tree ? 1 : G); c0 += FG_CHUNK) {  // (level 2: one pass over the 8 leaders)
 #pragma unroll
             for (int mm = 0; mm < FG_CHUNK; ++mm) {
-              pp[mm] = (tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr;
+              pp[mm] = tree ? (tid < CH ? slot(mm, e3) + GW_SUB3 + tid : nullptr)
+                            : ((tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr);
               tg[mm] = tag3;
             }
             if (c0 == 0 && mi >= 0) pp[0] = pat;
@@ -821,7 +851,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             if (tid < CH) {
 #pragma unroll
               for (int mm = 0; mm < FG_CHUNK; ++mm)
-                if (c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
+                if (tree || c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
             if (c0 == 0) {
               vat = __builtin_bit_cast(float, v[0]);
@@ -1095,10 +1125,35 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       TPROBE(10);
         // ---- P4 words: the moment record (11 doubles); consume every member's ----
         const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
-        if (tid < NMOM) gputd(slot(g, e4) + GW_P4 + 2 * tid, tag4, sm.dred[tid], l2);
-        {
+        if (tid < NMOM) gputd(slot(g, e4) + GW_P4 + 2 * tid, tag4, sm.dred[tid], tree ? sl2 : l2);
+        if (tree) {
+          // level 1 (leaders g < 8): the records of members g, g + 8, ... (<= 16: one word per thread), summed in member
+          // order (double) by wave 0's lanes j < NMOM and published write-through
+          if (g < 8) {
+            const int nsub = (G - g + 7) / 8, nw = 2 * NMOM * nsub;
+            const u64* pp[1] = {tid < nw ? slot(g + 8 * (tid / (2 * NMOM)), e4) + GW_P4 + tid % (2 * NMOM) : nullptr};
+            unsigned v[1];
+            gpoll<1>(pp, tag4, v, a);
+            if (tid < nw) sm.gw[tid] = v[0];
+            __syncthreads();
+            if (wave_s == 0) {
+              const double* gd = reinterpret_cast<const double*>(sm.gw);
+              double sj = 0.0;
+              const int j = lane < NMOM ? lane : 0;
+              for (int k = 0; k < nsub; ++k) sj += gd[NMOM * k + j];
+              if (lane < NMOM) gputd(slot(g, e4) + GW_SUB4 + 2 * lane, tag4, sj, false);
+            }
+            __syncthreads();  // the leader's words read before the leaders' partials land in sm.gw
+          }
+          // level 2 (everyone): the 8 leaders' partial records
+          const int nw = 2 * NMOM * 8;
+          const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_SUB4 + tid % (2 * NMOM) : nullptr};
+          unsigned v[1];
+          gpoll<1>(pp, tag4, v, a);
+          if (tid < nw) sm.gw[tid] = v[0];
+        } else {
           // word k % 22 of member k / 22: one word per thread up to 23 members; beyond, passes of up to four words in
-          // flight per thread (128 members: 2816 words, two passes)
+          // flight per thread (32 members: 704 words, one pass)
           const int nw = 2 * NMOM * G;
           if (nw <= NTHR) {
             const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_P4 + tid % (2 * NMOM) : nullptr};
@@ -1131,7 +1186,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         double sj = 0.0;
         {
           const int j = lane < NMOM ? lane : 0;
-          for (int mm = 0; mm < G; ++mm) sj += gd[NMOM * mm + j];
+          for (int mm = 0; mm < (tree ? 8 : G); ++mm) sj += gd[NMOM * mm + j];  // members, or the 8 leaders' partials
         }
         double ms[NMOM];
 #pragma unroll

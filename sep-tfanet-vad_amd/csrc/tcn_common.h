@@ -149,7 +149,11 @@ constexpr int GW_BOT = 4 + 4 * CH;  // P1: rows 32-dil..31  [dil][256]
 constexpr int GW_ROW = GW_BOT + 4 * CH;  // P3: per-channel sums over own frames [256]
 constexpr int GW_COL = GW_ROW + CH;      // P3: per-frame channel sums [32]
 constexpr int GW_P4 = 4;                 // P4: the moment record, 11 doubles as 22 words (clear of P2's GW_STAT)
-static_assert(GW_COL + FR <= NGR && GW_P4 >= GW_STAT + 4, "granule slot size / P2-P4 separation");
+// Two-level reductions of large groups (k_tcn, G > FG_TREE): the leaders' partial P3 row sums and P4 records, past
+// every P1 word (without TF-attention a block has three epochs, so P1 and P4 share a slot parity every other block)
+constexpr int GW_SUB3 = GW_COL + FR;     // [256] a leader's partial row sums
+constexpr int GW_SUB4 = GW_SUB3 + CH;    // [22] a leader's partial moment record
+static_assert(GW_SUB4 + 2 * NMOM <= NGR && GW_P4 >= GW_STAT + 4, "granule slot size / P2-P4 separation");
 
 
 // One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or
@@ -339,14 +343,18 @@ __device__ __forceinline__ KArgs kargs() {
   return p;
 }
 
-// {sum, sumsq} over the G members' statistic words (member mm: doubles 2mm, 2mm+1 of gw), member order;
-// lanes 0/1 of every wave load and add, the totals are returned wave-uniform
+// {sum, sumsq} over the G members' statistic words (member mm: doubles 2mm, 2mm+1 of gw), returned wave-uniform:
+// lane l of half h (h = 0: sums, 1: sums of squares) adds members l, l + 32, ... in order, then a fixed xor tree over
+// the half's 32 lanes; lanes 0 / 32 hold the results (a fixed order: bitwise reproducible). Large groups only (the
+// polling wave finishes groups up to FG_WAVE in member order, member_moments_w).
 __device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int lane) {
   const double* gd = reinterpret_cast<const double*>(gw);
-  const int j = lane & 1;
+  const int h = lane >> 5, l = lane & 31;
   double s = 0.0;
-  for (int mm = 0; mm < G; ++mm) s += gd[2 * mm + j];
-  return double2{readlane_d(s, 0), readlane_d(s, 1)};
+  for (int mm = l; mm < G; mm += 32) s += gd[2 * mm + h];
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  return double2{readlane_d(s, 0), readlane_d(s, 32)};
 }
 // GroupNorm {mean, rstd} from the statistic words polled by one wave: lane base + 4 mm + {0, 1, 2, 3} holds
 // member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane): the same
