@@ -150,7 +150,7 @@ struct sepvad_model {
   int split = 1;
   hipStream_t sub[MAX_SPLIT] = {};
   hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
-  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs are not fp32 and T <= 4096
+  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs are not fp32 and T <= 8192
   bool fused = true;
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU), max over precisions
   int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
@@ -972,7 +972,7 @@ int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, 
 
 namespace {
 
-// The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 32 * FG_MAX = 4096) and a group fits
+// The fused TCN runs when the GEMMs are fp16x3, an utterance fits one group (T <= 32 * FG_MAX = 8192) and a group fits
 // the co-resident capacity; otherwise the multi-kernel path below runs (same results within fp32 rounding).
 static_assert(SEPVAD_PREC_FP32 == PREC_F32 && SEPVAD_PREC_F16X3 == PREC_F16X3 && SEPVAD_PREC_F16 == PREC_F16 &&
               SEPVAD_PREC_BF16 == PREC_BF16, "precision codes");

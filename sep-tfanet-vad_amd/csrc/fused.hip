@@ -104,6 +104,14 @@ constexpr int PD = TCN_PD;        // weight K steps in flight per wave
 constexpr int NS1 = CH / 16;      // conv1d K steps (256 / 16)
 constexpr int NS2 = HID / 16;     // res_out K steps (512 / 16)
 
+// gathered words: 4 GN words per member, the flat moment records of up to FG_TREE members, a P4 tree leader's
+// subgroup records (<= ceil(FG_MAX / 8) members)
+constexpr int GW_WORDS = 4 * FG_MAX > 2 * NMOM * ((FG_MAX + 7) / 8) ? (4 * FG_MAX > 2 * NMOM * FG_TREE ? 4 * FG_MAX
+                                                                                                   : 2 * NMOM * FG_TREE)
+                                                                 : 2 * NMOM * ((FG_MAX + 7) / 8);
+static_assert(GW_WORDS >= 2 * NMOM * FG_TREE && GW_WORDS >= 2 * NMOM * 8 && GW_WORDS >= FG_MAX, "gathered words");
+static_assert(4 * FG_MAX <= 2 * NTHR, "GN words: at most two per thread");
+
 struct TcnSmem {
   _Float16 Ahi[FR * LDD];         // GEMM A operand, hi plane: x' [32][LDX] or d [32][LDD]
   _Float16 Alo[FR * LDD];         //                 lo plane
@@ -117,7 +125,7 @@ struct TcnSmem {
   float cs[FR][8];                // per-frame channel partial sums (8 channel slices)
   float csum[FR];                 // own per-frame channel sums
   float red[NMOM * 16];
-  unsigned gw[FG_MAX * 2 * NMOM] __attribute__((aligned(8)));  // gathered statistic words of all members
+  unsigned gw[GW_WORDS] __attribute__((aligned(8)));  // gathered statistic words (GN words, moment records)
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
@@ -291,8 +299,12 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   }
 }
 
-template <int LM, int PRE, bool DUMP = false, int LQ = 0, bool PROBE = false>
+template <int LM, int PRE, bool DUMP = false, int LQ = 0, bool PROBE = false, bool LG = false>
 __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
+  // LG: groups above FG_WAVE members (long utterances). The short instantiation (G <= FG_WAVE, every batch of
+  // utterances up to 16.4 s) compiles without the long groups' LDS word paths, wider polls and tree reductions:
+  // they cost cfg 2 3.6 % of its k_tcn cycles as uniform branches (registers / SGPR spills, profiles/r04ab_*)
+  static_assert(FG_TREE >= FG_WAVE, "tree reductions only in the long-group instantiation");
   // phase stamps only in the probe instantiation (SEPVAD_TCN_PROBE): none of their pointers or branches in production
   const bool TP_ON = PROBE && a.probe != nullptr;
   using WL = WLay<PRE, LQ>;
@@ -338,10 +350,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   }
   bool l2 = false;
   // groups above FG_TREE members reduce the P3 row sums and the P4 moment records in two levels: member g's words go
-  // to leader g % 8 (the members of one leader share blockIdx % 8, one XCD under round-robin dispatch: speed only),
-  // every member then polls the 8 leaders' partial sums -- 3 hand-off round trips instead of G / 8 (P3) and a 176-
-  // word poll instead of 22 G words (P4). sl2: the member and its leader share an XCD (checked at epoch 1)
-  const bool tree = G > FG_TREE;
+  // to leader g % 8 (above 32 members the group is dealt contiguously, so a leader's members share blockIdx % 8: one
+  // XCD under round-robin dispatch, speed only), every member then polls the 8 leaders' partial sums -- 3 hand-off
+  // round trips instead of G / 8 (P3) and a 176-word poll instead of 22 G words (P4). sl2: the member and its leader
+  // share an XCD (checked at epoch 1); the leaders' partials stay in L2 only when the whole group does (l2)
+  const bool tree = LG && G > FG_TREE;
   bool sl2 = false;
   const int T = a.T, Tp = a.Tp, t0 = g * FR;
   const bool tf = a.tf_att != 0;
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       bool same = a.xmode == 0, sub = a.xmode == 0;
       for (int mm = 0; mm < G; ++mm) {
         same = same && sm.gw[mm] == sm.gw[0];
-        sub = sub && (mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8]);
+        if (LG) sub = sub && (mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8]);
       }
       l2 = same;
       sl2 = sub;
@@ -544,8 +557,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       // ---- consume P1: neighbours' boundary rows -> H halo; every member's GN1 sums ----
       {
-        const u64* p[5];
-        unsigned v[5];
+        const u64* p[LG ? 6 : 5];
+        unsigned v[LG ? 6 : 5];
         int hrow[4], hcol[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -564,22 +577,25 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             }
           }
         }
-        const int sk = tid - (NTHR - 4 * G);  // last 4G threads: GN1 words of member sk/4
+        // GN1 words of member sk/4: the last 4G threads up to 128 members; above, thread t takes words t and t + 512
+        const int sk = !LG || 4 * G <= NTHR ? tid - (NTHR - 4 * G) : tid, sk2 = !LG || 4 * G <= NTHR ? -1 : tid + NTHR;
         p[4] = sk >= 0 ? slot(sk >> 2, e1) + GW_STAT + (sk & 3) : nullptr;
-        gpoll<5>(p, tag1, v, a);
+        if constexpr (LG) p[5] = sk2 >= 0 && sk2 < 4 * G ? slot(sk2 >> 2, e1) + GW_STAT + (sk2 & 3) : nullptr;
+        gpoll<LG ? 6 : 5>(p, tag1, v, a);
       TPROBE(3);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (hrow[k] >= 0) sm.H[hrow[k] * CH + hcol[k]] = p[k] != nullptr ? __builtin_bit_cast(float, v[k]) : 0.f;
 #if TCN_GNW
-        if (G <= FG_WAVE) {
+        if (!LG) {
           if (wave_s == NTHR / 64 - 1) {  // the GN1 pollers' wave: moments before the barrier
             float mu, rs;
             member_moments_w(v[4], 64 - 4 * G, G, a.inv_ch, 1e-8f, mu, rs);
             if (lane == 0) { sm.gmom[0] = mu; sm.gmom[1] = rs; }
           }
-        } else if (sk >= 0) {  // long utterances: the words span two waves, finished from LDS below
-          sm.gw[sk] = v[4];
+        } else {  // long utterances: the words span two waves or more, finished from LDS below
+          if (sk >= 0) sm.gw[sk] = v[4];
+          if constexpr (LG) if (p[5] != nullptr) sm.gw[sk2] = v[5];
         }
 #else
         if (sk >= 0) sm.gw[sk] = v[4];
@@ -598,7 +614,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float mu, rs;
         {
 #if TCN_GNW
-          if (G <= FG_WAVE) {
+          if (!LG) {
             mu = sm.gmom[0]; rs = sm.gmom[1];
           } else {  // same doubles in the same member order as member_moments_w
             const double2 acc = member_sums2(sm.gw, G, lane);
@@ -733,7 +749,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const unsigned e3 = tf ? ++ep : 0u, tag3 = a.tag0 + e3;
       // GN2 {mean, rstd} of the group from the polled P2 words (a wave's lanes base.. or the words in LDS)
       auto gn2_moments = [&](float& fmu, float& frs) {
-        if (G <= FG_WAVE) {
+        if (!LG) {
           fmu = sm.gmom[2]; frs = sm.gmom[3];
         } else {
           const double2 sums = member_sums2(sm.gw, G, lane);
@@ -741,17 +757,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
       };
       if (!tf) {  // no TF-attention sums to exchange: the P2 round alone
-        const u64* p[1] = {tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr};
-        unsigned v[1];
-        gpoll<1>(p, tag2, v, a);
-        if (G <= FG_WAVE) {
+        constexpr int NP2 = LG ? 2 : 1;
+        const u64* p[NP2];
+        unsigned v[NP2];
+        p[0] = tid < 4 * G ? slot(tid >> 2, e2) + GW_STAT + (tid & 3) : nullptr;
+        if constexpr (LG) p[1] = tid + NTHR < 4 * G ? slot((tid + NTHR) >> 2, e2) + GW_STAT + (tid & 3) : nullptr;
+        gpoll<LG ? 2 : 1>(p, tag2, v, a);
+        if (!LG) {
           if (wave_s == 0) {
             float mu, rs;
             member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
             if (lane == 0) { sm.gmom[2] = mu; sm.gmom[3] = rs; }
           }
-        } else if (tid < 4 * G) {
-          sm.gw[tid] = v[0];
+        } else {
+          if (tid < 4 * G) sm.gw[tid] = v[0];
+          if constexpr (LG) if (tid + NTHR < 4 * G) sm.gw[tid + NTHR] = v[NP2 - 1];
         }
         __syncthreads();
       TPROBE(6);
@@ -802,27 +822,28 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             const int tl = mi - 4, t = t0 + tl;
             if (t >= 0 && t < T) pat = tl < 0 ? slot(g - 1, e3) + GW_COL + tl + FR : slot(g + 1, e3) + GW_COL + tl - FR;
           }
-          // threads 384..: GN2 words kq + 128 j (j < 4) of the 4G (wave 6 holds all of them for G <= 16; up to 128
-          // members, 512 words, in the first pass's free slots)
+          // threads 384..: GN2 words kq + 128 j (j < 8) of the 4G (wave 6 holds all of them for G <= 16; up to 256
+          // members, 1024 words, in the first pass's free slots)
           const int kq = tid - (NTHR - 128);
           float s = 0.f, vat = 0.f;
-          unsigned vq[4] = {0u, 0u, 0u, 0u};
+          unsigned vq[FG_CHUNK] = {};
           if (tree) {
             // level 1 (leaders g < 8): the row sums of members g, g + 8, ..., member order, published write-through
             if (g < 8) {
+              constexpr int L1 = 16;  // subgroup members polled per pass (a subgroup has <= 16 up to 128 members)
               float ss = 0.f;
-              for (int c0 = g; c0 < G; c0 += 8 * FG_CHUNK) {
+              for (int c0 = g; c0 < G; c0 += 8 * L1) {
+                const u64* p1[L1];
+                unsigned v1[L1];
 #pragma unroll
-                for (int mm = 0; mm < FG_CHUNK; ++mm) {
-                  pp[mm] = (tid < CH && c0 + 8 * mm < G) ? slot(c0 + 8 * mm, e3) + GW_ROW + tid : nullptr;
-                  tg[mm] = tag3;
-                }
-                gpollt<FG_CHUNK>(pp, tg, v, a);
+                for (int mm = 0; mm < L1; ++mm)
+                  p1[mm] = (tid < CH && c0 + 8 * mm < G) ? slot(c0 + 8 * mm, e3) + GW_ROW + tid : nullptr;
+                gpoll<L1>(p1, tag3, v1, a);
 #pragma unroll
-                for (int mm = 0; mm < FG_CHUNK; ++mm)
-                  if (c0 + 8 * mm < G) ss += __builtin_bit_cast(float, v[mm]);
+                for (int mm = 0; mm < L1; ++mm)
+                  if (c0 + 8 * mm < G) ss += __builtin_bit_cast(float, v1[mm]);
               }
-              if (tid < CH) gputf(slot(g, e3) + GW_SUB3 + tid, tag3, ss, false);
+              if (tid < CH) gputf(slot(g, e3) + GW_SUB3 + tid, tag3, ss, l2);
             }
           }
           static_assert(FG_CHUNK == 8, "level 2 of the P3 tree polls the 8 leaders in one pass");
@@ -835,12 +856,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             }
             if (c0 == 0 && mi >= 0) pp[0] = pat;
             if (c0 == 0 && kq >= 0) {
-              if (G <= 32) {
+              if (!LG || G <= 32) {
                 pp[0] = kq < 4 * G ? slot(kq >> 2, e2) + GW_STAT + (kq & 3) : nullptr;
                 tg[0] = tag2;
               } else {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < FG_CHUNK; ++j) {
                   const int w = kq + 128 * j;
                   pp[j] = w < 4 * G ? slot(w >> 2, e2) + GW_STAT + (w & 3) : nullptr;
                   tg[j] = tag2;
@@ -856,10 +877,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             if (c0 == 0) {
               vat = __builtin_bit_cast(float, v[0]);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) vq[j] = v[j];
+              for (int j = 0; j < (LG ? FG_CHUNK : 1); ++j) vq[j] = v[j];
             }
           }
-          if (G <= FG_WAVE) {
+          if (!LG) {
             if (wave_s == 6) {
               float mu, rs;
               member_moments_w(vq[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
@@ -867,7 +888,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             }
           } else if (kq >= 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < FG_CHUNK; ++j)
               if (kq + 128 * j < 4 * G) sm.gw[kq + 128 * j] = vq[j];
           }
           __syncthreads();  // csum, the GN2 moments / words complete
@@ -895,7 +916,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         unsigned v[1];
         gpoll<1>(p, tag2, v, a);
 #if TCN_GNW
-        if (G <= FG_WAVE) {
+        if (!LG) {
           if (wave_s == 0) {  // the GN2 pollers' wave: moments before the barrier (eps rescaled with d)
             float mu, rs;
             member_moments_w(v[0], 0, G, a.inv_hid, pm[PB_EPS2], mu, rs);
@@ -916,7 +937,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float fmu, frs;
         {
 #if TCN_GNW
-          if (G <= FG_WAVE) {
+          if (!LG) {
             fmu = sm.gmom[2]; frs = sm.gmom[3];
           } else {
             const double2 acc = member_sums2(sm.gw, G, lane);
@@ -1130,18 +1151,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           // level 1 (leaders g < 8): the records of members g, g + 8, ... (<= 16: one word per thread), summed in member
           // order (double) by wave 0's lanes j < NMOM and published write-through
           if (g < 8) {
-            const int nsub = (G - g + 7) / 8, nw = 2 * NMOM * nsub;
-            const u64* pp[1] = {tid < nw ? slot(g + 8 * (tid / (2 * NMOM)), e4) + GW_P4 + tid % (2 * NMOM) : nullptr};
-            unsigned v[1];
-            gpoll<1>(pp, tag4, v, a);
+            const int nsub = (G - g + 7) / 8, nw = 2 * NMOM * nsub;  // <= 704 words (32 members)
+            const int k2 = tid + NTHR;
+            const u64* pp[2] = {tid < nw ? slot(g + 8 * (tid / (2 * NMOM)), e4) + GW_P4 + tid % (2 * NMOM) : nullptr,
+                                k2 < nw ? slot(g + 8 * (k2 / (2 * NMOM)), e4) + GW_P4 + k2 % (2 * NMOM) : nullptr};
+            unsigned v[2];
+            gpoll<2>(pp, tag4, v, a);
             if (tid < nw) sm.gw[tid] = v[0];
+            if (k2 < nw) sm.gw[k2] = v[1];
             __syncthreads();
             if (wave_s == 0) {
               const double* gd = reinterpret_cast<const double*>(sm.gw);
               double sj = 0.0;
               const int j = lane < NMOM ? lane : 0;
               for (int k = 0; k < nsub; ++k) sj += gd[NMOM * k + j];
-              if (lane < NMOM) gputd(slot(g, e4) + GW_SUB4 + 2 * lane, tag4, sj, false);
+              if (lane < NMOM) gputd(slot(g, e4) + GW_SUB4 + 2 * lane, tag4, sj, l2);
             }
             __syncthreads();  // the leader's words read before the leaders' partials land in sm.gw
           }
@@ -1155,7 +1179,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           // word k % 22 of member k / 22: one word per thread up to 23 members; beyond, passes of up to four words in
           // flight per thread (32 members: 704 words, one pass)
           const int nw = 2 * NMOM * G;
-          if (nw <= NTHR) {
+          if (!LG || nw <= NTHR) {
             const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_P4 + tid % (2 * NMOM) : nullptr};
             unsigned v[1];
             gpoll<1>(pp, tag4, v, a);
@@ -1457,30 +1481,35 @@ hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int PRE, int LQ>
+template <int PRE, int LQ, bool LG>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
   if constexpr (PRE == PREC_F16X3) {
     if (a.dump != nullptr) {  // parity-probe instantiation (the probe code stays out of the production kernels)
       switch (a.ln_mode) {
-        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
-        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, true, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, true, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
+        case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, true, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
     }
   }
   if (a.probe != nullptr && a.ln_mode == LD_RECURSIVE) {  // phase-stamp instantiation (SEPVAD_TCN_PROBE, recursive LN)
-    hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ, true>), dim3(grid), dim3(NTHR), 0, s, a);
+    hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ, true, LG>), dim3(grid), dim3(NTHR), 0, s, a);
     return hipGetLastError();
   }
   switch (a.ln_mode) {
-    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
-    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, false, LQ>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RECURSIVE: hipLaunchKernelGGL((k_tcn<LD_RECURSIVE, PRE, false, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_RESIDUAL: hipLaunchKernelGGL((k_tcn<LD_RESIDUAL, PRE, false, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
+    case LD_ADD: hipLaunchKernelGGL((k_tcn<LD_ADD, PRE, false, LQ, false, LG>), dim3(grid), dim3(NTHR), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <int PRE, int LQ>
+static hipError_t launch_tcn_lg(const TcnArgs& a, int grid, hipStream_t s) {
+  return a.G > FG_WAVE ? launch_tcn_pre<PRE, LQ, true>(a, grid, s) : launch_tcn_pre<PRE, LQ, false>(a, grid, s);
 }
 
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
@@ -1489,13 +1518,13 @@ hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
   switch (a.prec) {
     case PREC_F16X3:
       switch (a.lo8) {
-        case 0: return launch_tcn_pre<PREC_F16X3, 0>(a, grid, s);
-        case 1: return launch_tcn_pre<PREC_F16X3, 1>(a, grid, s);
-        case 2: return launch_tcn_pre<PREC_F16X3, 2>(a, grid, s);
+        case 0: return launch_tcn_lg<PREC_F16X3, 0>(a, grid, s);
+        case 1: return launch_tcn_lg<PREC_F16X3, 1>(a, grid, s);
+        case 2: return launch_tcn_lg<PREC_F16X3, 2>(a, grid, s);
       }
       return hipErrorInvalidValue;
-    case PREC_F16: return launch_tcn_pre<PREC_F16, 0>(a, grid, s);
-    case PREC_BF16: return launch_tcn_pre<PREC_BF16, 0>(a, grid, s);
+    case PREC_F16: return launch_tcn_lg<PREC_F16, 0>(a, grid, s);
+    case PREC_BF16: return launch_tcn_lg<PREC_BF16, 0>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }
@@ -1509,7 +1538,14 @@ static int blocks_per_cu_pre(int ln_mode) {
     case LD_RESIDUAL: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_RESIDUAL, PRE, false, LQ>, NTHR, 0); break;
     case LD_ADD: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tcn<LD_ADD, PRE, false, LQ>, NTHR, 0); break;
   }
-  return e == hipSuccess ? nb : 0;
+  int nl = 0;  // the long-group instantiation: the capacity is the smaller of the two (both 1 / CU by their LDS)
+  hipError_t el = hipErrorInvalidValue;
+  switch (ln_mode) {
+    case LD_RECURSIVE: el = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_tcn<LD_RECURSIVE, PRE, false, LQ, false, true>, NTHR, 0); break;
+    case LD_RESIDUAL: el = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_tcn<LD_RESIDUAL, PRE, false, LQ, false, true>, NTHR, 0); break;
+    case LD_ADD: el = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nl, k_tcn<LD_ADD, PRE, false, LQ, false, true>, NTHR, 0); break;
+  }
+  return e == hipSuccess && el == hipSuccess ? (nb < nl ? nb : nl) : 0;
 }
 
 int tcn_blocks_per_cu(int ln_mode, int prec, int lo) {

@@ -277,14 +277,17 @@ hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 // ---- fused persistent TCN (fused.hip) ----
 constexpr int FR = 32;          // frames per workgroup
 #ifndef SEPVAD_FG_MAX
-#define SEPVAD_FG_MAX 128
+#define SEPVAD_FG_MAX 256
 #endif
-constexpr int FG_MAX = SEPVAD_FG_MAX;  // workgroups per utterance (T <= 4096: 65.5 s at 16 kHz in one fused forward; groups
+constexpr int FG_MAX = SEPVAD_FG_MAX;  // workgroups per utterance (T <= 8192: 131 s at 16 kHz in one fused forward; groups
                                 // above 32 members span XCDs and hand off through write-through words)
 constexpr int FG_CHUNK = 8;     // members polled / summed per pass (register budget of the polls)
 constexpr int FG_WAVE = 16;     // groups up to this size keep the GN1/GN2 words in one wave (readlane finish)
 constexpr int NGR = 2624;       // 8-byte {tag, value} hand-off words per slot (P1 rows, P3 sums, tree partials: GW_*)
-constexpr int FG_TREE = 32;     // groups above this many members reduce P3 / P4 in two levels (8 leaders)
+#ifndef SEPVAD_FG_TREE
+#define SEPVAD_FG_TREE 16
+#endif
+constexpr int FG_TREE = SEPVAD_FG_TREE;     // groups above this many members reduce P3 / P4 in two levels (8 leaders)
 constexpr int TCN_EPOCH_BITS = 12;  // tag = launch salt << 12 | epoch; epochs per launch < 4096
 // Per-block parameter blob of the fused TCN (floats; staged into LDS once per block):
 constexpr int PB_WS1 = 0, PB_B1 = 256, PB_G1 = 512, PB_BE1 = 768;   // conv1d row scales, bias; reg1 affine

@@ -231,7 +231,8 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
 // (utterance, speaker): y[t][o] = sum_k P[t - 2 + k][4 k + o] (zero outside [0, T)), v = PReLU(y + b1),
 // BN_1 = GroupNorm(1, 4) over [4, T] (block sums in double, wave order), feat = v * s[o] + h[o] for
 // k_istft_pair's VAD tail (model/model.py:158-176).
-// NI items (t, o) per thread: 4 for T <= 256, 16 for T <= 1024, 64 for T <= 4096 (long utterances on the fused schedule).
+// NI items (t, o) per thread: 4 for T <= 256, 16 for T <= 1024, 64 for T <= 4096, 128 for T <= 8192 (long utterances on
+// the fused schedule).
 template <int NI>
 __global__ __launch_bounds__(256) void k_vad_feat(VadFeatArgs a) {
   __shared__ float red[2 * 16];
@@ -269,10 +270,11 @@ __global__ __launch_bounds__(256) void k_vad_feat(VadFeatArgs a) {
 }
 
 hipError_t launch_vad_feat(const VadFeatArgs& a, hipStream_t s) {
-  if (a.T < 1 || a.T > 4096) return hipErrorInvalidValue;
+  if (a.T < 1 || a.T > 8192) return hipErrorInvalidValue;
   if (a.T <= 256) hipLaunchKernelGGL(k_vad_feat<4>, dim3(a.B * 2), dim3(256), 0, s, a);
   else if (a.T <= 1024) hipLaunchKernelGGL(k_vad_feat<16>, dim3(a.B * 2), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_vad_feat<64>, dim3(a.B * 2), dim3(256), 0, s, a);
+  else if (a.T <= 4096) hipLaunchKernelGGL(k_vad_feat<64>, dim3(a.B * 2), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_vad_feat<128>, dim3(a.B * 2), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -131,19 +131,19 @@ def test_inference_kw_on_fused(nets):
 
 
 def test_long_utterances_fall_back(nets):
-    """T > 4096 (N >= 1048576, 65.5 s) does not fit one group of 128: the multi-kernel schedule runs."""
-    x = torch.rand(1, 1048576, device=DEV) * 1.8 - 0.9
+    """T > 8192 (N >= 2097152, 131 s) does not fit one group of 256: the multi-kernel schedule runs."""
+    x = torch.rand(1, 2097152, device=DEV) * 1.8 - 0.9
     _, _, _, used = _run(nets["with_vad"], x, True)
     assert not used
 
 
-@pytest.mark.parametrize("N", [262144, 480000, 960000, 1048320])
+@pytest.mark.parametrize("N", [262144, 480000, 960000, 1048320, 2000000, 2096896])
 def test_whole_file_forwards_stay_fused(N, nets, state_dicts):
-    """only_inference.py:90-91 forwards a whole file (model/model.py:402-461 has no length limit): 16.4 s, 30 s, 60 s and
-    65.5 s at 16 kHz are G = 33, 59, 118 and 128 workgroups per utterance -- groups that span XCDs (write-through
-    hand-offs), GN2 words polled in the first P3 pass's spare slots, moment words in 512-word passes; N = 1048320 is
-    T = 4096, the largest fused utterance (N = 1048576, T = 4097, is test_long_utterances_fall_back). Fused vs the
-    multi-kernel schedule and vs the oracle on utterance 0."""
+    """only_inference.py:90-91 forwards a whole file (model/model.py:402-461 has no length limit): 16.4 s, 30 s, 60 s,
+    65.5 s, 125 s and 131 s at 16 kHz are G = 33, 59, 118, 128, 245 and 256 workgroups per utterance -- groups that span
+    XCDs (write-through hand-offs), the two-level P3 / P4 reductions (8 leaders), GN words two per thread above 128
+    members; N = 2096896 is T = 8192, the largest fused utterance (N = 2097152, T = 8193, is
+    test_long_utterances_fall_back). Fused vs the multi-kernel schedule and vs the oracle on utterance 0."""
     from oracle.torch_ref import OracleModel
     from sep_tfanet_vad_amd import synth
     net = nets["with_vad"]
