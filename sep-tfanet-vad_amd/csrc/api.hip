@@ -70,7 +70,7 @@ struct Workspace {
   size_t bytes = 0;
   float2* X; float* specdb; float* S0; float* O[2]; float* A; float* R;
   float* masks; float* colsum; float* rowsum; float* at; float* af; float* vy; float* vad;
-  float* vP;  // [B][2][Tp][HEAD_VAD_N] VAD conv1_1 tap products from k_head (fused schedule)
+  float* vP;  // [B][2][Tp][HEAD_VAD_N] VAD conv1_1 tap products from k_tcn's output head (fused schedule)
   __half* Dhi; __half* Dlo; float* D32;  // res_out operand d (fp16 split planes, or fp32, same bytes)
   // partial records of the statistics producers (deterministic per-workgroup sums)
   double* rec_gate; double* rec_g1; double* rec_dw; double* rec_mom; double* rec_hs; double* rec_vad;
@@ -134,11 +134,12 @@ struct sepvad_model {
   size_t ln_g = 0, ln_b = 0;
   PackedW wout;
   size_t out_g = 0, out_b = 0, bo = 0;
-  // k_head's copy of the output head: speaker q's 257 rows at rows [288 q, 288 q + 257) (zero rows to 288), so a
-  // workgroup of 9 x 32 rows is one speaker; and the VAD conv1_1 as that workgroup's second GEMM (HEAD_VAD:
-  // B[c][4 k + o] = w1[o][c][k], 20 of 32 columns, 288 speaker-local channels)
+  // k_tcn's copy of the output head: speaker q's 257 rows at rows [288 q, 288 q + 257) (zero rows to 288); its MFMA
+  // tiles are rows [288 q, 288 q + 256), bin 256 of each speaker is out_ny (fp32 [2][CH] + bias [2]); the VAD conv1_1
+  // as a second GEMM on each masks tile (B[c][4 k + o] = w1[o][c][k], 20 of 32 columns, speaker-local channels
+  // c < 256; vad_ny[4 k + o] = w1[o][256][k])
   PackedW wout_spk, vadw;
-  size_t bo_spk = 0;
+  size_t bo_spk = 0, out_nyw = 0, out_nyb = 0, vad_ny = 0;
   float vad_sx = 1.f;  // fp16 range scale of the VAD GEMM's A operand (undone by vadw.scale)
   float out_a = 0.f;
   size_t v_w1 = 0, v_b1 = 0, v_g = 0, v_b = 0, v_w2 = 0;
@@ -570,10 +571,10 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
   if (h->tcn_cap > 0) {
     const size_t gb = (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long);
     HIPCHK(hipMalloc(&c->tgran, gb));
-    HIPCHK(hipMemset(c->tgran, 0, gb));
+    HIPCHK(hipMemsetAsync(c->tgran, 0, gb, (hipStream_t)stream));  // (ordered before this stream's first launch)
   }
   HIPCHK(hipMalloc(&c->terr, 16));
-  HIPCHK(hipMemset(c->terr, 0, 16));
+  HIPCHK(hipMemsetAsync(c->terr, 0, 16, (hipStream_t)stream));
   HIPCHK(hipHostMalloc((void**)&c->herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(c->herr, 0, 64);
   HIPCHK(hipHostGetDevicePointer((void**)&c->herr_dev, c->herr, 0));
@@ -613,6 +614,13 @@ int salt_reserve(sepvad_model* h, StreamCtx* c, hipStream_t s, unsigned n, unsig
 }
 
 int check_giveup(StreamCtx* c) {
+  if (env_int("SEPVAD_GIVEUP_INFO", 0) && (c->pending != 0 || (c->herr[0] != 0 && c->herr[0] != c->reported))) {
+    unsigned w[4] = {};  // diagnostics: {launch tag0, the timed-out wait's tag, its workgroup, its word index}
+    if (hipMemcpy(w, c->terr, sizeof(w), hipMemcpyDeviceToHost) == hipSuccess)
+      fprintf(stderr, "sepvad: give-up on stream %p: tag0 %#x, first timed-out wait: tag %#x (salt %u epoch %u) "
+              "workgroup %u word %u (slot %u, offset %u)\n", c->stream, w[0], w[1], w[1] >> TCN_EPOCH_BITS,
+              w[1] & ((1u << TCN_EPOCH_BITS) - 1), w[2], w[3], w[3] / NGR, w[3] % NGR);
+  }
   if (c->pending != 0) {
     c->pending = 0;
     return fail(SEPVAD_E_HIP, "fused TCN: a group hand-off wait gave up in an earlier forward on this stream "
@@ -826,6 +834,13 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
       }
     h->wout_spk = pack_pointwise(pk, ws, MOUT_PAD, CH, MOUT_PAD, eh);
     h->bo_spk = pk.add(bs);
+    std::vector<float> nyw((size_t)2 * CH), nyb(2);
+    for (int q = 0; q < 2; ++q) {
+      std::memcpy(&nyw[(size_t)q * CH], &wo[((size_t)q * NBIN + NBIN - 1) * CH], CH * sizeof(float));
+      nyb[q] = bb[q * NBIN + NBIN - 1];
+    }
+    h->out_nyw = pk.add(nyw);
+    h->out_nyb = pk.add(nyb);
   }
   // VAD head (model/model.py:153-171)
   if (c.final_vad) {
@@ -862,6 +877,10 @@ sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors
     const int ev_ = range_exp(mb);
     h->vad_sx = std::ldexp(1.f, -ev_);
     h->vadw = pack_pointwise(pk, wv, HEAD_VAD_N, HEAD_SPK, 32, ev_);
+    std::vector<float> vny(HEAD_VAD_N);
+    for (int o = 0; o < 4; ++o)
+      for (int k = 0; k < 5; ++k) vny[4 * k + o] = w1[((size_t)o * NBIN + NBIN - 1) * 5 + k];
+    h->vad_ny = pk.add(vny);
     h->v_b1 = pk.add(b1, 4);
     h->v_a = a[0];
     h->v_g = pk.add(gg, 4);
@@ -1005,9 +1024,15 @@ int tcn_order_big(int device, hipStream_t s, bool after) {
   static std::unordered_map<int, hipEvent_t> last;  // device -> the last big launch's completion
   std::lock_guard<std::mutex> lk(mu);
   hipEvent_t& e = last[device];
-  if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (after) HIPCHK(hipEventRecord(e, s));
-  else HIPCHK(hipStreamWaitEvent(s, e, 0));
+  if (after) {  // a fresh event per launch: a wait already enqueued never sees a later record of the same event
+    hipEvent_t n = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&n, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(n, s));
+    if (e) HIPCHK(hipEventDestroy(e));  // (released once its waits have completed)
+    e = n;
+  } else if (e) {
+    HIPCHK(hipStreamWaitEvent(s, e, 0));
+  }
   return SEPVAD_OK;
 }
 
@@ -1116,7 +1141,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   unsigned gsalt_lo = 0, gsalt_n = 0;  // salts of this chunk's k_tcn launches (give-up poisoning, k_istft_pair)
   h->last_fused = use_fused;
   const bool has_vad = c.final_vad && (!c.final_vad_masked_speakers || c.noisy_phase);
-  // the VAD conv1_1 as k_head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
+  // the VAD conv1_1 as the output head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
   const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
     // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
@@ -1142,6 +1167,17 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.dump_blk = std::max(0, std::min(h->nblk - 1, env_int("SEPVAD_TCN_DUMP_BLOCK", 0)));
     int ngroups = std::min(B, tcn_cap_of(h) / Gt);
     if (ngroups >= 8) ngroups -= ngroups % 8;
+    // the output head, inside k_tcn after each utterance's last block (its lo plane in the blocks' format)
+    ta.hg = h->P(h->out_g); ta.hbe = h->P(h->out_b); ta.hsx = h->out_sx;
+    ta.hwh = h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
+    ta.hwl = h->H(ta.lo8 == 2 ? h->wout_spk.fi8 : (ta.lo8 == 1 ? h->wout_spk.fl8 : h->wout_spk.flo));
+    ta.hwscale = h->P(h->wout_spk.scale); ta.hbias = h->P(h->bo_spk);
+    ta.hnyw = h->P(h->out_nyw); ta.hnyb = h->P(h->out_nyb);
+    if (vad_in_head) {
+      ta.hvwh = h->H(h->vadw.fhi); ta.hvwl = h->H(h->vadw.flo); ta.hvwscale = h->P(h->vadw.scale);
+      ta.hvny = h->P(h->vad_ny);
+      ta.hvsx = h->vad_sx;
+    }
     // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
     // counted as 4 (headroom)
     // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)
@@ -1166,8 +1202,8 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       ta.B = Bl;
       ta.S0 = w.S0 + (size_t)u0 * Tp * CH;
       ta.ln = gn_src(w.rec_gate + (size_t)u0 * (Tp / GATE_ROWS) * 2, Tp / GATE_ROWS, 2, 0, h->P(h->ln_g), h->P(h->ln_b), 1e-8f);
-      ta.Xfin = w.O[0] + (size_t)u0 * Tp * CH;
-      ta.rec_head = w.rec_hs + (size_t)u0 * Gt * 2;
+      ta.hmasks = w.masks + (size_t)u0 * Tp * MOUT_PAD;
+      ta.hvP = vad_in_head ? w.vP + (size_t)u0 * 2 * Tp * HEAD_VAD_N : nullptr;
       ta.probe = nullptr;
       ta.dump = (h->tdump && u0 == 0 && Bl == B) ? h->tdump : nullptr;
       if (probe_path && u0 == 0) {
@@ -1195,7 +1231,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       const bool big = tcn_big(h, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
       if (big && tcn_order_big(h->device, s, false)) return SEPVAD_E_HIP;
       if (ev()) return SEPVAD_E_HIP;
+      TailProbe thp(h, s, "tcnhead");
+      ta.hprobe = u0 == 0 ? thp.buf : nullptr;
       HIPCHK(launch_t(ta, ngl * Gt));
+      if (ta.hprobe) HIPCHK(thp.dump(ngl * Gt, 1));
       if (ev()) return SEPVAD_E_HIP;
       if (big && tcn_order_big(h->device, s, true)) return SEPVAD_E_HIP;
       if (tr) {
@@ -1216,28 +1255,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         }
       }
     }
-    // output head on the members' slices (k_head), then the eager masks_b copy if asked
-    HeadArgs ha{};
-    ha.B = B; ha.T = T; ha.Tp = Tp; ha.G = G; ha.prec = h->prec;
-    ha.Xfin = w.O[0]; ha.rec = w.rec_hs; ha.Grec = Gt;
-    ha.g = h->P(h->out_g); ha.be = h->P(h->out_b); ha.alpha = h->out_a; ha.sx = h->out_sx;
-    ha.inv_ch = 1.0 / ((double)CH * T);
-    ha.wh = h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
-    ha.wl = h->H(h->wout_spk.flo);
-    ha.wscale = h->P(h->wout_spk.scale); ha.bias = h->P(h->bo_spk);
-    ha.masks = w.masks;
-    if (vad_in_head) {
-      ha.vP = w.vP;
-      ha.vwh = h->H(h->vadw.fhi); ha.vwl = h->H(h->vadw.flo); ha.vwscale = h->P(h->vadw.scale);
-      ha.vsx = h->vad_sx;
-    }
-    if (ev()) return SEPVAD_E_HIP;
-    TailProbe tp(h, s, "head");
-    ha.probe = tp.buf;
-    HIPCHK(launch_head(ha, s));
-    HIPCHK(tp.dump(2LL * ha.B * ha.G, 1));
-    if (ev()) return SEPVAD_E_HIP;
-    if (tr) tr->gemm_ev.push_back((int)h->ev.size() - 2);
+    // the eager masks_b copy if asked
     if (out->masks_b) {
       MaskSideArgs m{};
       m.B = B; m.T = T; m.Tp = Tp; m.masks = w.masks; m.masks_b = out->masks_b + (size_t)b0 * MOUT * T;
@@ -1331,7 +1349,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     }
   }
   stage.next("sepvad::vad");
-  // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from k_head's tap products (k_vad_feat,
+  // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from the output head's tap products (k_vad_feat,
   // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
   // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, the same arithmetic; measured

@@ -50,9 +50,6 @@ namespace sepvad {
 #ifndef TCN_MOM5
 #define TCN_MOM5 1   // recursive-LN moment record from 5 per-thread row sums, channel weights applied once
 #endif
-#ifndef HEAD_VT_ALIAS
-#define HEAD_VT_ALIAS 1  // k_head's VAD tiles alias the A operand (40 KB LDS, one more barrier) or own LDS (74 KB)
-#endif
 #ifndef TCN_PFX
 #define TCN_PFX 1    // weight-ring prefetches interleaved with the rows of the phase before the GEMM (1) or in one burst (0)
 #endif
@@ -129,6 +126,10 @@ struct TcnSmem {
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
 };
+static_assert(offsetof(TcnSmem, Alo) == offsetof(TcnSmem, Ahi) + sizeof(TcnSmem::Ahi) &&
+              16 * FR * HEAD_VAD_N * 4 <= sizeof(TcnSmem::H) && 4 * FR * 32 * 2 <= FR * (LDD - LDX) &&
+              2 * FR <= 4 * CH,
+              "fused head: the waves' tap products in H, their VAD tiles in the A planes' unused row tails");
 static_assert(offsetof(TcnSmem, at) % 8 == 0 && offsetof(TcnSmem, H) % 8 == 0 && offsetof(TcnSmem, prm) % 16 == 0,
               "packed (8-byte) reads of at / H / the parameter blob");
 
@@ -1237,11 +1238,14 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         }
       if (TCN_SUB == 0) TPROBE(13);
       }
-      // next block's conv1d weights: in flight during the x' update
-      // (the last block re-reads its own weights: the loads stay unconditional and in bounds)
-      const __half* wn = bi + 1 < a.nblk ? wb + WL::BLOCK : wb;
-      const __amdgpu_buffer_rsrc_t wnh = rsrc_of(wn), wnl = rsrc_of(wn + WL::W1L);
-      if (!TCN_PFX && bi + 1 < a.nblk) prefetch_w<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl);
+      // next block's conv1d weights: in flight during the x' update; after the last block, the output head's first
+      // row tile (speaker 0, tile hjl: the head's wave -> tile map) instead
+      const bool lastb = bi + 1 == a.nblk;
+      const int hjl = (wave_s + (blockIdx.x >> 3)) & 7;
+      const __amdgpu_buffer_rsrc_t wnh = lastb ? rsrc_of(a.hwh) : rsrc_of(wb + WL::BLOCK);
+      const __amdgpu_buffer_rsrc_t wnl = lastb ? rsrc_of(PRE == PREC_F16X3 ? a.hwl : a.hwh) : rsrc_of(wb + WL::BLOCK + WL::W1L);
+      const int pvo = lastb ? (hjl * NS1 * 64 + lane) * 16 : voff1, pvol = lastb ? (hjl * (NS1 / 2) * 64 + lane) * 16 : voff1l;
+      if (!TCN_PFX) prefetch_w<PRE, RD, LQ>(wnh, wnl, pvo, pvol, rh, rl);
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
@@ -1251,7 +1255,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         for (int r = 0; r < 16; r += 2) {
 #pragma unroll
           for (int e = 0; e < RPI; ++e)
-            if (TCN_PFX) prefetch_w1<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl, RPI * (r / 2) + e);
+            if (TCN_PFX) prefetch_w1<PRE, RD, LQ>(wnh, wnl, pvo, pvol, rh, rl, RPI * (r / 2) + e);
           const int tl = trow(r);
           const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r], rv[r + 1]}, kc);  // rv gated above
           const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
@@ -1263,7 +1267,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE, RD, LQ>(wnh, wnl, voff1, voff1l, rh, rl, r / 2);
+          if (TCN_PFX && r % 2 == 0) prefetch_w1<PRE, RD, LQ>(wnh, wnl, pvo, pvol, rh, rl, r / 2);
           const int tl = trow(r);
           const float x = resid_apply<LM>(o[r], rv[r], 1.f, 0, kc, kc + 1, kc + 2, kc + 3);  // rv gated above
           o[r] = (t0 + tl < T) ? x : 0.f;
@@ -1274,24 +1278,181 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       __syncthreads();
       TPROBE(12);
     }
-    // ---- TCN output x' (head input) and the statistics of PReLU(x') for TCN.output.1 ----
+    // ---- output head (model/model.py:322-325,357): masks = W_out GN_out(PReLU(x')) + b on this member's slice, and
+    // the VAD conv1_1 tap products of the masks (model/model.py:158-160), while x' is still in registers (o). The
+    // statistics of PReLU(x') are one more hand-off round (P5). 16 row tiles of 32 on MFMA (speaker q's bins
+    // 32 jl .. 32 jl + 31, jl < 8), two per wave; bin 256 of each speaker (one row) as fp32 VALU dot products.
     {
-      const int tidt = fresh_tid(wave_s);
-      const int hl4t = 4 * ((tidt >> 5) & 1), mt_ = 32 * wave_s + (tidt & 31);
-      auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4t; };
-      float st[2] = {0.f, 0.f};
-      float* Xu = a.Xfin + ((size_t)u * Tp + t0) * CH;
+      const int tidh = fresh_tid(wave_s);
+      const int lh = tidh & 63, hl4h = 4 * ((tidh >> 5) & 1), mh = 32 * wave_s + (tidh & 31);
+      auto trow = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4h; };
+      // diagnostics (SEPVAD_TAIL_PROBE, first utterance): slot 0 wall clock, 1.. shader clock at the phase ends
+      unsigned long long* const hpr = a.hprobe != nullptr && u == grp ? a.hprobe + (size_t)blockIdx.x * 8 : nullptr;
+      auto hstamp = [&](int k) {
+        if (hpr != nullptr && tidh == 0) hpr[k] = __builtin_amdgcn_s_memtime();
+      };
+      if (hpr != nullptr && tidh == 0) hpr[0] = wall_clock64();
+      hstamp(1);
+      // the first tile's weights are in the ring since the last block's x' update (each next tile's are issued during
+      // the current tile's epilogue)
+      // (the weight copy keeps 9 row tiles per speaker: speaker q's tile jl is row tile HEAD_SPK / 32 * q + jl). The
+      // wave -> tile map rotates with the workgroup's place on its XCD, so the XCD's CUs stream different tiles at a
+      // time (speed only: every result is indexed by tile, not by wave)
+      const int jl = (wave_s + (blockIdx.x >> 3)) & 7;
+      auto tile_voff = [&](int q) { return ((q * (HEAD_SPK / 32) + jl) * NS1 * 64 + lh) * 16; };
+      auto tile_voffl = [&](int q) { return ((q * (HEAD_SPK / 32) + jl) * (NS1 / 2) * 64 + lh) * 16; };
+      const __amdgpu_buffer_rsrc_t wh = rsrc_of(a.hwh), wl = rsrc_of(PRE == PREC_F16X3 ? a.hwl : a.hwh);
+      // P5: the member's record of PReLU(x') (sum, sumsq over its valid frames), every member's in member order
+      {
+        float st[2] = {0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = t0 + trow(r);
-        if (t < Tp) st_out(Xu + trow(r) * CH + mt_, o[r]);
-        if (t < T) {
-          const float pv = prelu_f(o[r], a.alpha_h);
-          st[0] += pv; st[1] += pv * pv;
+        for (int r = 0; r < 16; ++r) {
+          if (t0 + trow(r) < T) {
+            const float pv = prelu_f(o[r], a.alpha_h);
+            st[0] += pv; st[1] += pv * pv;
+          }
+        }
+        block_sums<2>(st, sm.red, sm.dred);
+      }
+      const unsigned e5 = ++ep, tag5 = a.tag0 + e5;  // (P4 is a full round before: no member still polls GW_STAT)
+      if (tidh < 2) gputd(slot(g, e5) + GW_STAT + 2 * tidh, tag5, sm.dred[tidh], l2);  // (the thread's own sum)
+      {
+        constexpr int NP = LG ? 2 : 1;
+        const u64* p[NP];
+        unsigned v[NP];
+        p[0] = tidh < 4 * G ? slot(tidh >> 2, e5) + GW_STAT + (tidh & 3) : nullptr;
+        if constexpr (LG) p[NP - 1] = tidh + NTHR < 4 * G ? slot((tidh + NTHR) >> 2, e5) + GW_STAT + (tidh & 3) : nullptr;
+        gpoll<NP>(p, tag5, v, a);
+        if (tidh < 4 * G) sm.gw[tidh] = v[0];
+        if constexpr (LG) if (tidh + NTHR < 4 * G) sm.gw[tidh + NTHR] = v[NP - 1];
+      }
+      hstamp(2);
+      __syncthreads();
+      if (tidh < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in member order
+        const double* gd = reinterpret_cast<const double*>(sm.gw);
+        double sd = 0.0;
+        for (int mm = 0; mm < G; ++mm) sd += gd[2 * mm + tidh];
+        sm.dred[8 + tidh] = sd;
+      }
+      __syncthreads();
+      // A = GN_out(PReLU(x')) into LDS (scaled by hsx, undone by the weights' row scale)
+      {
+        float mu, rs;
+        gn_moments_f(sm.dred[8], sm.dred[9], a.inv_ch, 1e-5f, mu, rs);
+        const float sc = rs * a.hg[mh], sh = a.hbe[mh] - sc * mu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          split_store<PRE>(sm.Ahi, sm.Alo, trow(r) * LDX + mh, fmaf(prelu_f(o[r], a.alpha_h), sc, sh) * a.hsx);
+      }
+      __syncthreads();  // A complete
+      hstamp(3);
+      const bool vad = a.hvP != nullptr;
+      // this wave's VAD tile: [32 frames][32 channels], 16-B granules XOR-swizzled by frame, in the unused tail of
+      // the A planes (row stride LDD, only LDX in use); the waves' tap products [8][2][FR][20] in H (free now)
+      float* const vsc = reinterpret_cast<float*>((wave_s < 4 ? sm.Ahi : sm.Alo) + FR * LDX) + (wave_s & 3) * FR * 32;
+      float* const Ps = sm.H;
+      auto vidx = [](int t, int c) { return t * 32 + ((((c >> 2) ^ t) & 7) << 2) + (c & 3); };
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int jt = q * (HEAD_SPK / 32) + jl;  // row tile of the weight copy
+        f32x16v acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        wave_gemm<NS1, LDX, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, wh, wl, tile_voff(q), tile_voffl(q), rh, rl, lh);
+        if (q == 0) prefetch_w<PRE, RD, LQ>(wh, wl, tile_voff(1), tile_voffl(1), rh, rl);
+        f16x8 vb[2][2];
+        if (vad) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            vb[st][0] = *reinterpret_cast<const f16x8*>(a.hvwh + ((size_t)(2 * jl + st) * 64 + lh) * 8);
+            vb[st][1] = *reinterpret_cast<const f16x8*>(a.hvwl + ((size_t)(2 * jl + st) * 64 + lh) * 8);
+          }
+        }
+        const int c = 32 * jl + (lh & 31);  // speaker-local bin
+        const float ws = a.hwscale[32 * jt + (lh & 31)], bias = a.hbias[32 * jt + (lh & 31)];
+        float* const out = a.hmasks + ((size_t)u * Tp + t0) * MOUT_PAD + q * NBIN + c;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[r] = fmaf(acc[r], ws, bias);
+          st_out(out + (size_t)trow(r) * MOUT_PAD, acc[r]);
+        }
+        if (vad) {  // VAD conv1_1 tap products of the tile's 32 bins: P[t][n] = sum_c masks[t][c] Wv[c][n], fp16x3
+#pragma unroll
+          for (int r = 0; r < 16; ++r) vsc[vidx(trow(r), lh & 31)] = acc[r] * a.hvsx;
+          wave_lds_sync();
+          f32x16v pv;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pv[r] = 0.f;
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int tr = lh & 31, c0 = 16 * st + 8 * (lh >> 5);
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(vsc + vidx(tr, c0));
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(vsc + vidx(tr, c0 + 4));
+            f16x8 ah, al;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = e < 4 ? x0[e] : x1[e - 4];
+              const _Float16 hh = (_Float16)x;
+              ah[e] = hh;
+              al[e] = (_Float16)(x - (float)hh);
+            }
+            pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, vb[st][0], pv, 0, 0, 0);
+            pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][1], pv, 0, 0, 0);
+            pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][0], pv, 0, 0, 0);
+          }
+          wave_lds_sync();  // the tile's reads done before the wave's next tile overwrites it
+          if ((lh & 31) < HEAD_VAD_N) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Ps[((jl * 2 + q) * FR + trow(r)) * HEAD_VAD_N + (lh & 31)] = pv[r];
+          }
         }
       }
-      block_sums<2>(st, sm.red, a.rec_head + ((size_t)u * G + g) * 2);
-      __syncthreads();
+      hstamp(4);
+      // bin 256 of each speaker (one row, fp32 VALU) from A in LDS: thread -> (speaker, frame, 32-channel part),
+      // channels in order, then the 8 parts by a fixed xor tree (while slower waves finish their tiles)
+      float* const nys = &sm.c[0][0];  // [2][FR] (c is free)
+      {
+        const int od = tidh >> 3, part = tidh & 7, qn = od >> 5, tn = od & 31;
+        const _Float16* ah = sm.Ahi + tn * LDX + 32 * part;
+        const _Float16* al = sm.Alo + tn * LDX + 32 * part;
+        const f32x4* wq = reinterpret_cast<const f32x4*>(a.hnyw + qn * CH + 32 * part);
+        float sn = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f16x8 hv = *reinterpret_cast<const f16x8*>(ah + 8 * k);
+          f16x8 lv = {};
+          if constexpr (PRE == PREC_F16X3) lv = *reinterpret_cast<const f16x8*>(al + 8 * k);
+          const f32x4 w0 = wq[2 * k], w1 = wq[2 * k + 1];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x;
+            if constexpr (PRE == PREC_BF16) x = (float)__builtin_bit_cast(__bf16, hv[e]);
+            else x = PRE == PREC_F16X3 ? (float)hv[e] + (float)lv[e] : (float)hv[e];
+            sn = fmaf(x, e < 4 ? w0[e] : w1[e - 4], sn);
+          }
+        }
+        sn += __shfl_xor(sn, 1);
+        sn += __shfl_xor(sn, 2);
+        sn += __shfl_xor(sn, 4);
+        if (part == 0) nys[qn * FR + tn] = sn / a.hsx + a.hnyb[qn];  // (hsx: a power of two)
+      }
+      __syncthreads();  // bin 256 and every wave's tap products in LDS
+      // the tap products: the tiles' in tile order, then bin 256's term (fp32)
+      for (int i = tidh; i < (vad ? 2 * FR * HEAD_VAD_N : 2 * FR); i += NTHR) {
+        const int per = vad ? FR * HEAD_VAD_N : FR;
+        const int q = i >= per ? 1 : 0, ri = i - q * per;
+        const int t = vad ? ri / HEAD_VAD_N : ri, n = vad ? ri - t * HEAD_VAD_N : 0;
+        const float m = nys[q * FR + t];
+        if (n == 0) st_out(a.hmasks + ((size_t)u * Tp + t0 + t) * MOUT_PAD + q * NBIN + (NBIN - 1), m);
+        if (vad) {
+          float sum = 0.f;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) sum += Ps[((w * 2 + q) * FR + t) * HEAD_VAD_N + n];  // tile order
+          a.hvP[(((size_t)u * 2 + q) * Tp + t0) * HEAD_VAD_N + ri] = t0 + t < T ? fmaf(m, a.hvny[n], sum * a.hvwscale[n]) : 0.f;
+        }
+      }
+      hstamp(5);
+      __syncthreads();  // (the next utterance's prologue rewrites the LDS)
     }
   }
   // (the clock record pointer re-read from the kernarg segment: nothing held in registers across the blocks)
@@ -1300,185 +1461,6 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (blockIdx.x == 0) { ck[3] = rt; ck[5] = __builtin_amdgcn_s_memtime(); }
     __hip_atomic_fetch_max(ck + 1, rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// ------------------------------------------------------------------------------------------
-// k_head: TCN.output (model/model.py:322-325,357) on the fused schedule, with the VAD head's conv1_1
-// (model/model.py:158-160) as a second GEMM on the masks tile. Two workgroups per 32-frame slice of an
-// utterance (the k_tcn members' slices), one per speaker: 9 waves x one tile of 32 of the speaker's 288 rows
-// (257 + zero rows; the per-speaker weight copy wout_spk). A = GN_out(PReLU(x')) of the slice into LDS once
-// (statistics from k_tcn's per-member records, fixed order), each wave streams its tile's weights from L2 in
-// fragment order (wave_gemm) and stores its channels of the masks rows. VAD (a.vP): each wave transposes
-// its 32 x 32 masks tile through LDS into the A operand of P_w = tile . Wv (Wv[c][4k+o] = w1[o][c][k],
-// fp16x3 on v_mfma_f32_32x32x16_f16), the 9 partial P are summed in wave order and stored per frame (20
-// tap products); k_vad_feat finishes the conv (shifted tap sums + bias + PReLU) and BN_1. Together they
-// replace k_vad1 and its 18 MB re-read of the masks.
-constexpr int HTHR = 576;
-constexpr int HVLD = 33;  // row stride (floats) of a wave's masks / P tile in LDS
-template <int PRE>
-__global__ __launch_bounds__(HTHR, 6) void k_head(HeadArgs a) {
-#if HEAD_VT_ALIAS
-  // the VAD tiles of waves 0..7 reuse the A operand's bytes once every wave's GEMM is done (40 KB of LDS)
-  constexpr int AB = 2 * FR * LDX;  // halves: Ahi then Alo
-  static_assert(8 * FR * HVLD * 4 <= AB * 2, "8 VAD tiles fit the A operand's bytes");
-  __shared__ __attribute__((aligned(16))) _Float16 ab[AB];
-  __shared__ __attribute__((aligned(16))) float vt8[FR * HVLD];  // wave 8's VAD tile
-  _Float16* const Ahi = ab;
-  _Float16* const Alo = ab + FR * LDX;
-#else
-  // own VAD tiles, no barrier before them: 74 KB of LDS, and then only one workgroup per CU is resident
-  // (measured, r02aq: 21.6 vs 19.1 us)
-  __shared__ __attribute__((aligned(16))) _Float16 Ahi[FR * LDX];
-  __shared__ __attribute__((aligned(16))) _Float16 Alo[PRE == PREC_F16X3 ? FR * LDX : 8];
-  __shared__ __attribute__((aligned(16))) float vts[9][FR * HVLD];
-#endif
-  __shared__ float hs[2][CH];
-  __shared__ double dred[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sl = blockIdx.x >> 1, q = blockIdx.x & 1;  // slice, speaker
-  const int u = sl / a.G, g = sl % a.G, t0 = g * FR;
-  const int j = 9 * q + wave;  // this wave's row tile of wout_spk: speaker-local rows [32 wave, 32 wave + 32)
-  // diagnostics: slot 0 wall clock at entry, slots 1.. shader clock at the phase ends
-  unsigned long long* const pr = a.probe ? a.probe + (size_t)blockIdx.x * 8 : nullptr;
-  auto stamp = [&](int k) {
-    if (pr && tid == 0) pr[k] = __builtin_amdgcn_s_memtime();
-  };
-  if (pr && tid == 0) pr[0] = wall_clock64();
-  stamp(1);
-  // raw x' of the slice: 32 rows x 256 channels, thread-contiguous channels (coalesced 1 KB rows)
-  constexpr int NV = FR * CH / HTHR + 1;  // 15
-  float xv[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int i = tid + k * HTHR;
-    xv[k] = i < FR * CH ? a.Xfin[((size_t)u * a.Tp + t0) * CH + i] : 0.f;
-  }
-  if (tid < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in order
-    double s = 0.0;
-    for (int c0 = 0; c0 < a.Grec; c0 += FG_CHUNK) {
-      double v[FG_CHUNK];
-#pragma unroll
-      for (int mm = 0; mm < FG_CHUNK; ++mm) v[mm] = c0 + mm < a.Grec ? a.rec[((size_t)u * a.Grec + c0 + mm) * 2 + tid] : 0.0;
-#pragma unroll
-      for (int mm = 0; mm < FG_CHUNK; ++mm)
-        if (c0 + mm < a.Grec) s += v[mm];
-    }
-    dred[tid] = s;
-  }
-  __syncthreads();
-  stamp(2);
-  if (tid < CH) {
-    float mu, rs;
-    gn_moments_f(dred[0], dred[1], a.inv_ch, 1e-5f, mu, rs);
-    const float sc = rs * a.g[tid];
-    hs[0][tid] = sc;
-    hs[1][tid] = a.be[tid] - sc * mu;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int i = tid + k * HTHR;
-    if (i < FR * CH) {
-      const int r = i / CH, c = i % CH;
-      const float v = fmaf(prelu_f(xv[k], a.alpha), hs[0][c], hs[1][c]);
-      split_store<PRE>(Ahi, Alo, r * LDX + c, v * a.sx);
-    }
-  }
-  __syncthreads();
-  stamp(3);
-  // the tile's weight ring (issued here, not in the prologue: the register budget of 5 waves per SIMD;
-  // the co-resident workgroup's GEMM covers this one's prologue)
-  const __amdgpu_buffer_rsrc_t wh = rsrc_of(a.wh), wl = rsrc_of(PRE == PREC_F16X3 ? a.wl : a.wh);
-  const int voff = (j * NS1 * 64 + lane) * 16;
-  constexpr int HRD = 4;  // ring depth (k_tcn uses PD = 8 at 2 waves per SIMD)
-  u32x4v rh[HRD], rl[HRD];
-  prefetch_w<PRE, HRD>(wh, wl, voff, 0, rh, rl);
-  const int hl4 = 4 * (lane >> 5);
-  f32x16v acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  wave_gemm<NS1, LDX, PRE, HRD>(acc, Ahi, Alo, wh, wl, voff, 0, rh, rl, lane);
-  stamp(4);
-  // the VAD GEMM's B fragments (this wave's two K steps, hi and lo), in flight during the mask stores
-  f16x8 vb[2][2];
-  if (a.vP != nullptr) {
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      vb[st][0] = *reinterpret_cast<const f16x8*>(a.vwh + ((size_t)(2 * wave + st) * 64 + lane) * 8);
-      vb[st][1] = *reinterpret_cast<const f16x8*>(a.vwl + ((size_t)(2 * wave + st) * 64 + lane) * 8);
-    }
-  }
-  const int c = 32 * wave + (lane & 31);  // speaker-local channel (rows >= 257 are zero rows)
-  const float ws = a.wscale[32 * j + (lane & 31)], bias = a.bias[32 * j + (lane & 31)];
-  float* out = a.masks + ((size_t)u * a.Tp + t0) * MOUT_PAD + q * NBIN + c;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc[r] = fmaf(acc[r], ws, bias);
-    if (c < NBIN) st_out(out + (size_t)((r & 3) + 8 * (r >> 2) + hl4) * MOUT_PAD, acc[r]);
-  }
-  if (a.vP == nullptr) {
-    stamp(5);
-    return;
-  }
-#if HEAD_VT_ALIAS
-  float* const vtb = reinterpret_cast<float*>(ab);
-  auto vtile = [&](int w) { return w < 8 ? vtb + w * FR * HVLD : vt8; };
-  __syncthreads();  // every wave's GEMM has read A: its bytes become the VAD tiles
-#else
-  auto vtile = [&](int w) { return vts[w]; };
-#endif
-  float* tile = vtile(wave);
-#pragma unroll
-  for (int r = 0; r < 16; ++r)  // (range guard of the VAD GEMM's fp16 split)
-    tile[((r & 3) + 8 * (r >> 2) + hl4) * HVLD + (lane & 31)] = acc[r] * a.vsx;
-  // ---- VAD conv1_1 tap products of this wave's 32 channels: P_w[t][n] = sum_c tile[t][c] Wv[c][n] ----
-  wave_lds_sync();
-  f32x16v pv;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) pv[r] = 0.f;
-  {
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {  // K = 32 channels = 2 steps of 16
-      const float* ar = tile + (lane & 31) * HVLD + 16 * st + 8 * (lane >> 5);
-      f16x8 ah, al;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = ar[e];
-        const _Float16 h = (_Float16)x;
-        ah[e] = h;
-        al[e] = (_Float16)(x - (float)h);
-      }
-      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, vb[st][0], pv, 0, 0, 0);
-      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][1], pv, 0, 0, 0);
-      pv = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, vb[st][0], pv, 0, 0, 0);
-    }
-  }
-  wave_lds_sync();  // every lane's tile reads done before the partial P overwrites the tile
-#pragma unroll
-  for (int r = 0; r < 16; ++r) tile[((r & 3) + 8 * (r >> 2) + hl4) * HVLD + (lane & 31)] = pv[r];
-  __syncthreads();
-  float* vp = a.vP + (((size_t)u * 2 + q) * a.Tp + t0) * HEAD_VAD_N;
-  for (int i = tid; i < FR * HEAD_VAD_N; i += HTHR) {
-    const int t = i / HEAD_VAD_N, n = i - t * HEAD_VAD_N;
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 9; ++w) sum += vtile(w)[t * HVLD + n];  // wave (channel) order
-    vp[i] = t0 + t < a.T ? sum * a.vwscale[n] : 0.f;  // conv zero padding outside [0, T)
-  }
-  stamp(5);
-}
-
-hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
-  if (a.G < 1 || a.G * FR > a.Tp) return hipErrorInvalidValue;
-  static_assert(2 * 9 * 32 == MOUT_PAD && HEAD_SPK == 9 * 32, "one workgroup of 9 x 32 rows per speaker");
-  const dim3 grid(2 * a.B * a.G);
-  switch (a.prec) {
-    case PREC_F16X3: hipLaunchKernelGGL(k_head<PREC_F16X3>, grid, dim3(HTHR), 0, s, a); break;
-    case PREC_F16: hipLaunchKernelGGL(k_head<PREC_F16>, grid, dim3(HTHR), 0, s, a); break;
-    case PREC_BF16: hipLaunchKernelGGL(k_head<PREC_BF16>, grid, dim3(HTHR), 0, s, a); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 template <int PRE, int LQ, bool LG>

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
     mr[1][j] = a.masks[row * MOUT_PAD + NBIN + k];
   }
   constexpr int NQ = IP_FR + 6;
-  // VAD conv1_1 from k_head's tap products (vP mode, model/model.py:158-160): y[t][o] = sum_k P[t-2+k][4k+o]
+  // VAD conv1_1 from the output head's tap products (vP mode, model/model.py:158-160): y[t][o] = sum_k P[t-2+k][4k+o]
   // (zero outside [0, T)), v = PReLU(y + b1[o]) — k_vad_feat's arithmetic, expression for expression
   const bool taps = vad && a.vP != nullptr;
   auto tap_v = [&](const float* P, int i, int t, int o) {

@@ -21,7 +21,7 @@ constexpr int HID = 512;    // H_dim (depthwise multiplier 2)
 constexpr int TILE = 64;    // GEMM tile edge; Tp is a multiple of TILE
 constexpr int MOUT = 2 * NBIN;  // 514 output-head rows (2 speakers x 257 bins)
 constexpr int MOUT_PAD = 576;   // padded to a multiple of 64 (also the row stride of `masks`)
-constexpr int HEAD_SPK = MOUT_PAD / 2;  // k_head's per-speaker row block (257 rows + zero rows)
+constexpr int HEAD_SPK = MOUT_PAD / 2;  // the output head's per-speaker row block (257 rows + zero rows)
 constexpr int HEAD_VAD_N = 20;          // VAD conv1_1 tap products per frame: 5 taps x 4 outputs
 constexpr int SPEC_LD = 260;    // row stride of the frame-major dB spectrum
 constexpr int STAT_ROWS = 8;    // rows (frames) per workgroup of the stats kernels
@@ -177,7 +177,7 @@ struct Vad1Args {        // VAD conv1_1 (257->4, k=5) + bias + PReLU and GN(1,4)
   unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
 };
 
-struct VadFeatArgs {     // k_vad_feat: conv1_1 finish + BN_1 from k_head's tap products
+struct VadFeatArgs {     // k_vad_feat: conv1_1 finish + BN_1 from the output head's tap products
   int B, T, Tp;
   const float* vP;       // [B][2][Tp][HEAD_VAD_N]
   const float* b1; float alpha;       // conv1_1 bias [4], relu_1 PReLU
@@ -198,7 +198,7 @@ struct IstftArgs {
   float thr;
   const float* vy;       // [B][S][4][Tp] PReLU(conv1_1) output (k_vad1), or BN_1-normalised (vy_norm)
   int vy_norm;           // vy already normalised (k_vad_feat): no BN_1 records
-  const float* vP;       // nullable: k_head's conv1_1 tap products [B][2][Tp][HEAD_VAD_N]; the workgroup finishes
+  const float* vP;       // nullable: the output head's conv1_1 tap products [B][2][Tp][HEAD_VAD_N]; the workgroup finishes
                          // conv1_1 + PReLU + BN_1 itself (k_vad_feat's arithmetic, no vy / records)
   const float* vb1; float valpha;     // conv1_1 bias [4], relu_1 PReLU (vP mode)
   GnSrc vgn;             // BN_1 = GroupNorm(1, 4) over [4, T] per (utterance, speaker); rec [B*S][..]
@@ -320,8 +320,6 @@ struct TcnArgs {
   const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
   GnSrc ln;              // TCN.LN statistics records (k_gate) + affine
   float alpha_h;         // TCN.output.0 PReLU
-  float* Xfin;           // [B][Tp][CH] TCN output x' (head input)
-  double* rec_head;      // [B][G][2] (sum, sumsq) of PReLU(x') per member
   unsigned long long* gran;  // hand-off words [grid][2][NGR]
   unsigned tag0;         // launch salt << TCN_EPOCH_BITS (tags of this launch: tag0 + epoch, epoch >= 1)
   unsigned* err;         // device word: tag0 of the last launch on this stream context whose hand-off wait gave up
@@ -338,30 +336,23 @@ struct TcnArgs {
                          // block 0's res_out output r and its TF-attention output r * a_f * a_t
   unsigned dbg_delay;    // diagnostics (SEPVAD_TCN_DELAY): member 0 of each group sleeps before its polls (0: off)
   int dump_blk;          // parity probe: the block whose input (dump slot 0 when > 0), r and r a_f a_t are dumped
+  // output head after each utterance's last block (model/model.py:322-325,357): PReLU -> GroupNorm(1e-5) -> 1x1
+  // 256 -> 514 on the member's slice, and the VAD conv1_1 tap products of the masks (model/model.py:158-160)
+  float* hmasks;         // [B][Tp][MOUT_PAD] pre-sigmoid masks, speaker q's bins at [q * 257, q * 257 + 257)
+  const float* hg; const float* hbe;  // TCN.output.1 affine
+  float hsx;             // range scale of the head's A operand (undone by hwscale)
+  const __half* hwh; const __half* hwl;  // speaker-padded rows (288 per speaker), fragment order, the blocks' lo format
+  const float* hwscale; const float* hbias;  // [MOUT_PAD]
+  const float* hnyw; const float* hnyb;  // bin 256 of each speaker (fp32 VALU): weights [2][CH], bias [2]
+  // VAD conv1_1 as a second GEMM on each masks tile (nullable hvP: off): hvP[b][s][t][4 k + o] =
+  // sum_c masks[t][s 257 + c] w1[o][c][k], zero for t >= T; B planes in fragment order, per-column scale; bin 256's
+  // term w1[o][256][k] (hvny[4 k + o]) in fp32
+  const __half* hvwh; const __half* hvwl; const float* hvwscale; const float* hvny;
+  float hvsx;            // range scale of the masks tile as the VAD GEMM's A operand (undone by hvwscale)
+  float* hvP;            // nullable [B][2][Tp][HEAD_VAD_N]
+  unsigned long long* hprobe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [grid][8] fused-head phase stamps
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
-// Output head of the fused schedule (k_head): PReLU -> GroupNorm(1e-5) -> 1x1 256->514 (model/model.py:322-325,357)
-// for one 32-frame slice per workgroup, weights streamed in MFMA fragment order (as k_tcn).
-struct HeadArgs {
-  int B, T, Tp, G, prec;
-  const float* Xfin;     // [B][Tp][CH] TCN output x'
-  const double* rec;     // [B][Grec][2] (sum, sumsq) of PReLU(x') per k_tcn member
-  int Grec;              // records per utterance (k_tcn's workgroups per utterance)
-  const float* g; const float* be;  // TCN.output.1 affine
-  float alpha;           // TCN.output.0 PReLU
-  float sx;              // range scale of the A operand (undone by wscale)
-  double inv_ch;         // 1 / (CH * T)
-  const __half* wh; const __half* wl;  // fragment-ordered W planes [MOUT_PAD/32][CH/16][64][8] (wl: F16X3 only)
-  const float* wscale; const float* bias;  // [MOUT_PAD]
-  float* masks;          // [B][Tp][MOUT_PAD]
-  // VAD conv1_1 as a second GEMM on the masks tile (nullable vP: off): vP[b][s][t][4 k + o] =
-  // sum_c masks[t][s 257 + c] w1[o][c][k], zero for t >= T; B planes in fragment order, per-column scale
-  const __half* vwh; const __half* vwl; const float* vwscale;
-  float vsx;             // range scale of the masks tile as the VAD GEMM's A operand (undone by vwscale)
-  float* vP;             // [B][2][Tp][HEAD_VAD_N]
-  unsigned long long* probe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [workgroups][8] phase stamps
-};
-hipError_t launch_head(const HeadArgs& a, hipStream_t s);
 int tcn_blocks_per_cu(int ln_mode, int prec, int lo);
 // host: float -> e4m3fn (OCP FP8, bias 7, max 448, no inf), round to nearest even, saturating
 uint8_t e4m3_rn(float x);

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
   stamp(5);
 }
 
-// k_vad_feat: the VAD head's conv1_1 finished from k_head's tap products (fused schedule), one workgroup per
+// k_vad_feat: the VAD head's conv1_1 finished from the output head's tap products (k_tcn) (fused schedule), one workgroup per
 // (utterance, speaker): y[t][o] = sum_k P[t - 2 + k][4 k + o] (zero outside [0, T)), v = PReLU(y + b1),
 // BN_1 = GroupNorm(1, 4) over [4, T] (block sums in double, wave order), feat = v * s[o] + h[o] for
 // k_istft_pair's VAD tail (model/model.py:158-176).

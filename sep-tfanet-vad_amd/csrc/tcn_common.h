@@ -12,6 +12,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Wave-uniform copies (readfirstlane) of values loaded from the block-parameter table: the compiler cannot
 // prove those loads uniform, and a buffer descriptor in VGPRs becomes a waterfall loop per access.
@@ -94,6 +95,19 @@ __device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned 
     __builtin_amdgcn_s_sleep(1);
     if ((++spins & 255u) == 0 &&
         (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
+      if (spins > a.spin_limit) {  // diagnostics: the first timed-out wait of the launch {tag, workgroup, word}
+        int k0 = 0;
+#pragma unroll
+        for (int k = N - 1; k >= 0; --k)
+          if (p[k] != nullptr && (unsigned)(x[k] >> 32) != tag[k]) k0 = k;
+        unsigned z = 0;
+        if (__hip_atomic_compare_exchange_strong(a.err + 1, &z, tag[k0], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(a.err + 2, blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err + 3, (unsigned)((p[k0] - a.gran) & 0xffffffffu), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       giveup(a);
       return;
     }

@@ -4,7 +4,7 @@ reference goldens and the multi-kernel schedule, over the group sizes it support
 
 Tolerances: separated waveforms max-abs <= 1e-4 vs the reference/oracle (north_star); the two
 schedules differ only in the order of fp32 partial sums, so the waveforms agree to 1e-5. The VAD
-probabilities agree to 1e-4: the fused schedule computes the VAD conv1_1 as k_head's second GEMM (fp16x3
+probabilities agree to 1e-4: the fused schedule computes the VAD conv1_1 as the output head's second GEMM (fp16x3
 MFMA, channel sums in MFMA order), the other with k_vad1 (VALU, lane-tree order), and the VAD head
 amplifies rounding (tests/test_oracle_golden.py::test_reference_vad_sensitivity).
 """
@@ -186,7 +186,7 @@ def test_handoff_protocols_bitwise_identical(nets):
 
 
 def test_vad_taps_finished_in_istft(nets):
-    """SEPVAD_VAD_FEAT=0: k_istft_pair finishes the VAD conv1_1 + BN_1 from k_head's tap products itself
+    """SEPVAD_VAD_FEAT=0: k_istft_pair finishes the VAD conv1_1 + BN_1 from the output head's tap products itself
     (k_vad_feat's arithmetic); same results as the k_vad_feat schedule up to fp32 rounding, reference-pinned."""
     import os
     from sep_tfanet_vad_amd import synth
@@ -223,3 +223,28 @@ def test_long_files_full_chip_groups(nets, state_dicts):
     s_ref, v_ref, _ = om(x[:1])
     assert np.abs(sf[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
     check_vad_labels(vf[:1].cpu().numpy(), v_ref.numpy())
+
+
+@pytest.mark.parametrize("cname,B,N,sub", [("with_vad", 70, 32000, [0, 64, 69]), ("without_vad", 66, 32000, [1, 65]),
+                                            ("with_vad", 3, 256000, [2])])
+def test_output_head_in_tcn_vs_oracle(cname, B, N, sub, nets, state_dicts):
+    """The output head runs inside k_tcn after each utterance's last block (a second utterance per group when
+    B > 64 groups; 32-member groups at 16 s): masks_b (pre-sigmoid, all 514 rows) against the fp32 oracle, with
+    bin 256 of each speaker (fp32 VALU dot products, not MFMA) checked on its own, and the separated waveforms."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    net = nets[cname]
+    x = torch.from_numpy(synth.make_batch(B, N, 4242 + N)[0])
+    sf, vf, _, used = _run(net, x.to(DEV), True)
+    assert used
+    mb = net.masks_b.cpu().numpy()[sub]
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    s_ref, v_ref, _ = om(x[sub])
+    ref = om.masks_b.numpy()
+    err = np.abs(mb - ref).max()
+    err_ny = np.abs(mb[:, [256, 513]] - ref[:, [256, 513]]).max()
+    print(f"masks_b max-abs vs oracle {err:.2e} (bin 256: {err_ny:.2e})")
+    assert err <= 2e-4 and err_ny <= 2e-4
+    assert np.abs(sf.cpu().numpy()[sub] - s_ref.numpy()).max() <= SEP_TOL
+    if vf is not None and cname == "with_vad":
+        check_vad_labels(vf.cpu().numpy()[sub], v_ref.numpy())

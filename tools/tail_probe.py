@@ -12,6 +12,7 @@ import numpy as np
 NAMES = {"istft": ["loads + X sigmoid(m) rows", "VAD tail", "side outputs + transforms", "overlap-add"],
          "stft": ["loads + transform (wave 0)", "split + dB (wave 0)", "barrier", "activity gate + records"],
          "head": ["x' loads + records", "GN affine + A (LDS)", "GEMM (wave 0)", "mask stores issued"],
+         "tcnhead": ["P5 publish + poll", "records + GN + A (LDS)", "tiles (wave 0)", "tap sums + stores"],
          "vad1": ["loads + taps (FMA)", "lane reduction", "wave partials + barrier", "PReLU + features + records"]}
 
 
