@@ -57,9 +57,10 @@ def res_out_flops(B, T):
 
 
 def tcn_flops(B, T, precision="f16x3", nblk=24):
-    """Algorithmic FLOPs of one fused-TCN launch: the two pointwise GEMMs of every block (SURVEY §8d,
-    F_gemm without the output head): 24 * 2 * (256*256 + 512*256) per frame."""
-    return nblk * 2 * (256 * 256 + 512 * 256) * B * T
+    """Algorithmic FLOPs of one fused-TCN launch: the two pointwise GEMMs of every block and the output head that
+    runs inside the launch since round 4 (SURVEY §8d F_gemm): (24 * 2 * (256*256 + 512*256) + 2 * 514 * 256) per
+    frame."""
+    return (nblk * 2 * (256 * 256 + 512 * 256) + 2 * 514 * 256) * B * T
 
 
 def weight_bytes(precision, wlo="f16"):
@@ -68,16 +69,22 @@ def weight_bytes(precision, wlo="f16"):
     return (4 if wlo == "f16" else 3) if precision == "f16x3" else 2
 
 
+HEAD_ROWS_MFMA = 512  # output-head rows on MFMA inside k_tcn (bins 0..255 of 2 speakers; bin 256 on VALU)
+
+
 def tcn_bytes(B, T, precision="f16x3", wlo="f16"):
-    """Compulsory HBM bytes of one fused-TCN launch: TCN input read + output written (fp32 [B][Tp][256]),
-    the weights in fragment order read once (24 blocks x 768 KB as fp16 hi/lo, 576 KB with a byte lo plane,
-    384 KB as one 16-bit plane)."""
-    Tp = (T + 63) // 64 * 64
+    """Compulsory HBM bytes of one fused-TCN launch: TCN input read (fp32 [B][Tp][256]), the head's masks written
+    (fp32, 514 of [B][Tp][576]) and its VAD tap products ([B][2][Tp][20]), the weights in fragment order read once
+    (24 blocks x 768 KB as fp16 hi/lo, 576 KB with a byte lo plane, 384 KB as one 16-bit plane; the head's 512 MFMA
+    rows likewise)."""
+    Tp = (T + 31) // 32 * 32
     wbytes = weight_bytes(precision, wlo)
-    return 2 * B * Tp * 256 * 4 + 24 * (256 * 256 + 256 * 512) * wbytes
+    return (B * Tp * 256 * 4 + B * Tp * 514 * 4 + B * 2 * Tp * 20 * 4
+            + (24 * (256 * 256 + 256 * 512) + HEAD_ROWS_MFMA * 256) * wbytes)
 
 
-TA_FILE = "r02as_pmc_ta_summary.txt"   # texture-path counters of k_tcn (tools/pmc_ta.sh), cfg 2, f16x3
+TA_FILE = "r04prof_pmc_ta_summary.txt"  # texture-path counters of k_tcn (tools/r04_profile.sh), cfg 2, f16x3, i8 lo
+CACHE_FILE = "r04prof_coexec_tcc_dram.txt"  # MFMA/VALU co-issue, L2 hit/miss and memory-side read counters
 RING_FILE = "r02bi_ring_gemm.txt"       # GEMM-phase stream floor per CU (tools/probe_src/ring_gemm.hip)
 STREAM_FLOOR_GBPS = 103.2
 
@@ -96,7 +103,7 @@ def weight_stream(B, T, precision, avg_launch_s, n_cu=256, wlo="f16"):
            "floor_GBps_per_cu": STREAM_FLOOR_GBPS, "frac_of_floor": round(rate / STREAM_FLOOR_GBPS, 3),
            "floor_source": "profiles/" + RING_FILE, "ta_busy_frac": None, "ta_source": None}
     path = os.path.join(REPO, "profiles", TA_FILE)
-    if precision == "f16x3" and wlo == "f16" and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
+    if precision == "f16x3" and wlo == PMC_WLO and B == B_PER_GPU and T == 1 + N_SAMPLES // 256 and os.path.exists(path):
         try:
             lines = open(path).read().splitlines()
             i = next(k for k, ln in enumerate(lines) if "k_tcn" in ln)
@@ -108,6 +115,35 @@ def weight_stream(B, T, precision, avg_launch_s, n_cu=256, wlo="f16"):
     return out
 
 
+def cache_counters(wlo):
+    """k_tcn's L2 hit rate, MFMA/VALU co-issue and the attribution of `traffic` from the committed counter passes
+    (profiles/CACHE_FILE, headline configuration). The L2's memory-side reads count as DRAM-bound whether the
+    Infinity Cache serves them or not (TCC_EA0_RDREQ_DRAM_sum == TCC_EA0_RDREQ_sum), so the IC / HBM split is a
+    model: every XCD's L2 fetches each block's weights once (the weights stay IC-resident: 19.3 MB of 256 MB)."""
+    out = {"source": "profiles/" + CACHE_FILE}
+    try:
+        lines = open(os.path.join(REPO, "profiles", CACHE_FILE)).read().splitlines()
+        vals = {}
+        for i, ln in enumerate(lines):
+            if "k_tcn" in ln and i + 1 < len(lines):
+                vals.update(dict(t.split("=") for t in lines[i + 1].split()))
+        hit, miss = float(vals["TCC_HIT_sum"]), float(vals["TCC_MISS_sum"])
+        out["l2_hit_rate"] = round(hit / (hit + miss), 4)
+        out["mfma_busy_coissued_with_valu"] = round(float(vals["SQ_VALU_MFMA_COEXEC_CYCLES"])
+                                                    / float(vals["SQ_VALU_MFMA_BUSY_CYCLES"]), 3)
+        out["dram_bound_share_of_l2_reads"] = round(float(vals["TCC_EA0_RDREQ_DRAM_sum"])
+                                                    / float(vals["TCC_EA0_RDREQ_sum"]), 3)
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        pass
+    w = (24 * (256 * 256 + 256 * 512) + HEAD_ROWS_MFMA * 256) * weight_bytes("f16x3", wlo)
+    out["weights_bytes"] = w
+    out["model"] = {"per_xcd_weight_fetch_bytes": 8 * w, "ic_served_upper_bound_bytes": 7 * w,
+                    "note": "8 XCD L2s each fetch the launch's weights once; all but one copy can come from the "
+                            "Infinity Cache (upper bound on IC-served bytes); the rest of `traffic` is activations "
+                            "and hand-off words"}
+    return out
+
+
 def res_out_bytes(B, T):
     """Compulsory bytes of one res_out launch: operand d as fp16 hi+lo planes (B*Tp x 512 x 4 B),
     output r fp32 (B*Tp x 256 x 4 B), fp16 hi/lo weights (256 x 512 x 4 B)."""
@@ -115,8 +151,8 @@ def res_out_bytes(B, T):
     return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
 
 
-STATS_FILE = "r03ab_kernel_stats.csv"    # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
-TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false>"  # the dominant kernel's name in that file
+STATS_FILE = "r04prof_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
+TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false, false>"  # the dominant kernel's name in that file
 
 
 def rocprof_avg_us(kernel_prefix):
@@ -134,7 +170,7 @@ def rocprof_avg_us(kernel_prefix):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r03ab_pmc_tcn.json"       # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r04prof_pmc_tcn.json"     # fused schedule (k_tcn)
 PMC_WLO = "i8"                             # ... measured with this weight lo plane
 DEFAULT_SPLIT = 1
 
@@ -422,7 +458,7 @@ def main():
             # dominant kernel = the fused persistent TCN (all 24 blocks in one launch)
             flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision, args.wlo)
             body = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
-                    "512->256, TF-attention, recursive LN], ")
+                    "512->256, TF-attention, recursive LN] + output head 256->514 and VAD conv1_1 taps, ")
             if args.precision == "f16x3":
                 peak = F16_MFMA_PEAK_TFLOPS / 3.0
                 kern = body + "fp16x3 split on v_mfma_f32_32x32x16_f16: peak = 2.5 PF/s / 3)"
@@ -442,7 +478,7 @@ def main():
                 peak, kern = FP32_MFMA_PEAK_TFLOPS, ("k_gemm<F32,LD_PLAIN,EP_BIAS_ATT> (DepthConv1d.res_out 512->256, "
                                                      "v_mfma_f32_32x32x2_f32)")
         achieved = flops_launch / res_avg_s / 1e12
-        fwd_timed = n_gemm / (2 if fused else 2 * 24 + 1)  # GEMM-bearing launches per forward
+        fwd_timed = n_gemm / (1 if fused else 2 * 24 + 1)  # GEMM-bearing launches per forward
         all_gemm_tflops = gemm_flops_per_utt(T) * B * fwd_timed / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
         # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
         # (tools/gpu_round.sh -> tools/pmc.py; FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md corrections)
@@ -505,6 +541,8 @@ def main():
         }
         if fused:
             out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s, wlo=args.wlo)
+            if args.precision == "f16x3" and args.wlo == PMC_WLO and B == B_PER_GPU and N == N_SAMPLES:
+                out["roofline"]["caches"] = cache_counters(args.wlo)
             # the same fraction from the committed rocprofv3 average of the kernel (headline configuration only)
             if args.precision == "f16x3" and args.wlo == PMC_WLO and B == B_PER_GPU and N == N_SAMPLES:
                 rp = rocprof_avg_us(TCN_KERNEL_PREFIX)
