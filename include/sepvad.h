@@ -145,7 +145,7 @@ int32_t sepvad_forward_windows(sepvad_handle h, const float* x, int64_t ld_strea
 int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit);
 
 /* Select the TCN schedule of later forwards: 1 (default, or env SEPVAD_FUSED) = the whole separator stack
- * as one persistent launch when the GEMMs are F16X3 / F16 / BF16 and T <= 4096 (groups of ceil(T/32) <= 128 workgroups per
+ * as one persistent launch when the GEMMs are F16X3 / F16 / BF16 and T <= 8192 (groups of ceil(T/32) <= 256 workgroups per
  * utterance); 0 = one launch per stage (4 per block). Both meet the same parity gates. */
 int32_t sepvad_set_fused(sepvad_handle h, int32_t on);
 /* Synchronises the device and reports the schedule of the last forward and the persistent launch's

@@ -17,4 +17,6 @@ run offline_f16x3 \
 && SEPVAD_FUSED=0 run long30_multikernel --no-cpu-baseline --workload long --samples 480000 --batch 4 \
 && run long60_f16x3 --no-cpu-baseline --workload long --samples 960000 --batch 2 \
 && run offline_wlo_i8 --no-cpu-baseline --wlo i8 \
-&& run offline_wlo_e4m3 --no-cpu-baseline --wlo e4m3
+&& run offline_wlo_e4m3 --no-cpu-baseline --wlo e4m3 \
+&& run long125_f16x3 --no-cpu-baseline --workload long --samples 2000000 --batch 1 \
+&& run long125_b2_f16x3 --no-cpu-baseline --workload long --samples 2000000 --batch 2
