@@ -389,7 +389,10 @@ int ws_reserve(StreamCtx* c, int B, int N) {
   const size_t oVp = take(bt * 2 * HEAD_VAD_N * 4);
   char* base = nullptr;
   HIPCHK(hipMalloc(&base, off));
-  HIPCHK(hipMemset(base, 0, off));
+  // zeroed on the context's own stream, ahead of the forward that reserved it: a null-stream hipMemset is not
+  // ordered with a non-blocking caller stream, and once zeroed the workspace of a concurrent forward's first launch
+  // mid-run (tests/test_gpu_boundary.py::test_two_streams_concurrently_match_serial, round 4)
+  HIPCHK(hipMemsetAsync(base, 0, off, (hipStream_t)c->stream));
   w.base = base; w.bytes = off; w.Bmax = Bm; w.Tpmax = Tm;
   w.X = (float2*)(base + oX); w.specdb = (float*)(base + oSpec); w.S0 = (float*)(base + oS0);
   w.O[0] = (float*)(base + oO0); w.O[1] = (float*)(base + oO1); w.A = (float*)(base + oA);

@@ -1419,17 +1419,22 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         float sn = 0.f;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const f16x8 hv = *reinterpret_cast<const f16x8*>(ah + 8 * k);
-          f16x8 lv = {};
-          if constexpr (PRE == PREC_F16X3) lv = *reinterpret_cast<const f16x8*>(al + 8 * k);
+          // (read as the type split_store wrote: bf16 planes through __bf16, fp16 through _Float16)
+          float xv[8];
+          if constexpr (PRE == PREC_BF16) {
+            const bf16x8 bv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(ah) + 8 * k);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = (float)bv[e];
+          } else {
+            const f16x8 hv = *reinterpret_cast<const f16x8*>(ah + 8 * k);
+            f16x8 lv = {};
+            if constexpr (PRE == PREC_F16X3) lv = *reinterpret_cast<const f16x8*>(al + 8 * k);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = PRE == PREC_F16X3 ? (float)hv[e] + (float)lv[e] : (float)hv[e];
+          }
           const f32x4 w0 = wq[2 * k], w1 = wq[2 * k + 1];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float x;
-            if constexpr (PRE == PREC_BF16) x = (float)__builtin_bit_cast(__bf16, hv[e]);
-            else x = PRE == PREC_F16X3 ? (float)hv[e] + (float)lv[e] : (float)hv[e];
-            sn = fmaf(x, e < 4 ? w0[e] : w1[e - 4], sn);
-          }
+          for (int e = 0; e < 8; ++e) sn = fmaf(xv[e], e < 4 ? w0[e] : w1[e - 4], sn);
         }
         sn += __shfl_xor(sn, 1);
         sn += __shfl_xor(sn, 2);

@@ -58,10 +58,17 @@ def test_two_streams_concurrently_match_serial(net):
         outs.append((a, b))
     torch.cuda.synchronize()
     assert h.fused_status()
-    for a, b in outs:
+    bad = []
+    for i, (a, b) in enumerate(outs):
         for k in ("sep", "vad", "est"):
-            assert torch.equal(a[k], r1[k]), k
-            assert torch.equal(b[k], r2[k]), k
+            for name, got, ref in (("x1", a[k], r1[k]), ("x2", b[k], r2[k])):
+                if not torch.equal(got, ref):  # where: utterances, and the first / last differing sample or frame
+                    d = (got != ref).reshape(got.shape[0], -1)
+                    utts = torch.nonzero(d.any(dim=1)).flatten().tolist()
+                    idx = torch.nonzero(d[utts[0]]).flatten()
+                    bad.append(f"round {i} {name} {k}: utterances {utts}, utt {utts[0]} positions {idx[0].item()}.."
+                               f"{idx[-1].item()} of {d.shape[1]}, max abs {(got - ref).abs().max().item():.3e}")
+    assert not bad, "\n".join(bad)
 
 
 def test_giveup_is_reported_once_and_not_sticky(net):
