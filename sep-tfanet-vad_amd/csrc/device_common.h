@@ -28,6 +28,21 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 }
 
 __device__ __forceinline__ float prelu_f(float x, float w) { return x > 0.f ? x : w * x; }
+
+#ifndef SEPVAD_DB_FAST
+#define SEPVAD_DB_FAST 1
+#endif
+// 10 log10(clamp(|X|^2, 1e-10)) of one STFT bin (AmplitudeToDB of the power spectrum, model/model.py:17-25). Fast
+// form: |X|^2 as x^2 + y^2 and the logarithm through the hardware log2 (v_log_f32, ~1 ulp): within ~2e-5 dB of the
+// hypot / log10 form; every dB of the forward and of the side attribute takes the same form.
+__device__ __forceinline__ float power_db(float2 X) {
+#if SEPVAD_DB_FAST
+  return 3.01029995663981195f * __builtin_amdgcn_logf(fmaxf(fmaf(X.x, X.x, X.y * X.y), 1e-10f));
+#else
+  const float mag = hypotf(X.x, X.y);  // torch.abs(complex)
+  return 10.f * log10f(fmaxf(mag * mag, 1e-10f));
+#endif
+}
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
 // Workgroup barrier that orders LDS only. __syncthreads() carries a workgroup-scope fence, which hipcc

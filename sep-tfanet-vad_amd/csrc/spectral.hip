@@ -77,8 +77,7 @@ __global__ __launch_bounds__(256) void k_stft(StftArgs a) {
         Xk = cadd(E, cmul(tw[k], O));
       }
       if (k == 0) Xk = make_float2(0.f, 0.f);       // DC removed (model/model.py:24,410)
-      const float mag = hypotf(Xk.x, Xk.y);         // torch.abs(complex)
-      const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
+      const float db = power_db(Xk);
       if (live) {
         if (a.X) a.X[row * NBIN + k] = Xk;
         if (a.specdb) a.specdb[row * SPEC_LD + k] = db;

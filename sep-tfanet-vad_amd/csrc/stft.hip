@@ -106,8 +106,7 @@ __global__ __launch_bounds__(SG_THREADS) void k_stft_gate(StftArgs a) {
       const size_t xrow = (size_t)b * a.Tp + f;
       auto emit = [&](int k, float2 Xk) {
         if (k == 0) Xk = make_float2(0.f, 0.f);  // DC removed (model/model.py:24,410)
-        const float mag = hypotf(Xk.x, Xk.y);     // torch.abs(complex)
-        const float db = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
+        const float db = power_db(Xk);
         if (store_x && own) st_out(a.X + xrow * NBIN + k, Xk);
         if (store_db) {
           S[fi][k + 1] = live ? db : 0.f;

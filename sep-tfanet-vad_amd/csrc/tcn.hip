@@ -32,8 +32,7 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs a) {
     if (t >= 0 && t < T && f >= 0 && f < NBIN) {
       if (a.X != nullptr) {  // side pass: the forward's dB spectrum, recomputed bitwise from the stored STFT
         const float2 Xk = a.X[((size_t)b * a.Tp + t) * NBIN + f];
-        const float mag = hypotf(Xk.x, Xk.y);
-        v = 10.f * log10f(fmaxf(mag * mag, 1e-10f));
+        v = power_db(Xk);
       } else {
         v = a.specdb[((size_t)b * a.Tp + t) * SPEC_LD + f];
       }
