@@ -502,8 +502,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            # arithmetic type of the path: fp32 (fp16x3 is an fp32-equivalent split), or the reduced arm's operand
-            "dtype": {"f16x3": "fp32", "fp32": "fp32", "bf16": "bf16", "f16": "f16"}[args.precision],
+            # arithmetic type of the path's GEMMs: the fp16x3 split (fp32-accurate by measurement, not IEEE fp32: the
+            # weight lo plane keeps steps of 2^-19 of each row's largest weight), exact fp32
+            # (v_mfma_f32_32x32x2_f32), or the reduced arm's operand; everything outside the GEMMs is fp32
+            "dtype": {"f16x3": "f16x3 (fp32-accurate)", "fp32": "fp32", "bf16": "bf16", "f16": "f16"}[args.precision],
+            "ieee_fp32": args.precision == "fp32",
             "gemm_arithmetic": args.precision + (f" (weight lo plane {args.wlo})" if args.precision == "f16x3" else ""),
             "split": args.split,
             "schedule": "fused" if fused else "multi-kernel",

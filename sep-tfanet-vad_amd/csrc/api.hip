@@ -403,6 +403,8 @@ int ws_reserve(StreamCtx* c, int B, int N) {
   w.rec_gate = (double*)(base + oRg); w.rec_g1 = (double*)(base + oR1); w.rec_dw = (double*)(base + oRd);
   w.rec_mom = (double*)(base + oRm); w.rec_hs = (double*)(base + oRh); w.rec_vad = (double*)(base + oRv);
   w.vP = (float*)(base + oVp);
+  // the zeroing is this context's latest work: eviction (get_ctx) drains `done` before freeing the buffers
+  if (c->done) HIPCHK(hipEventRecord(c->done, (hipStream_t)c->stream));
   return SEPVAD_OK;
 }
 
@@ -581,6 +583,8 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
   HIPCHK(hipHostMalloc((void**)&c->herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(c->herr, 0, 64);
   HIPCHK(hipHostGetDevicePointer((void**)&c->herr_dev, c->herr, 0));
+  // the async zeroing above is already enqueued work of this context: an eviction before its first forward drains it
+  HIPCHK(hipEventRecord(c->done, (hipStream_t)stream));
   if (h->res_B > 0) {
     const int rc = ws_reserve(c.get(), h->res_B, h->res_N);
     if (rc) return rc;
@@ -623,6 +627,9 @@ int check_giveup(StreamCtx* c) {
       fprintf(stderr, "sepvad: give-up on stream %p: tag0 %#x, first timed-out wait: tag %#x (salt %u epoch %u) "
               "workgroup %u word %u (slot %u, offset %u)\n", c->stream, w[0], w[1], w[1] >> TCN_EPOCH_BITS,
               w[1] & ((1u << TCN_EPOCH_BITS) - 1), w[2], w[3], w[3] / NGR, w[3] % NGR);
+    // reported: clear the diagnostic words (the first timed-out poller sets them by a compare-and-swap from 0), so a
+    // later give-up on this context reports its own wait, not this one's
+    (void)hipMemsetAsync(c->terr + 1, 0, 3 * sizeof(unsigned), (hipStream_t)c->stream);
   }
   if (c->pending != 0) {
     c->pending = 0;
@@ -1022,20 +1029,23 @@ int env_int(const char* name, int dflt) {
 // completion event (stream-ordered, no host sync). Launches of small groups need no ordering: any resident prefix
 // of 8 G workgroups completes them, beside a big launch too, and they free their CUs.
 bool tcn_big(const sepvad_model* h, int G) { return 8 * G > tcn_cap_of(h) / 2; }
-int tcn_order_big(int device, hipStream_t s, bool after) {
+// Runs `launch` (which enqueues one big k_tcn launch on s) behind the previous big launch of the device and records
+// its completion as the next one's wait, all under one process-wide lock: two handles (or two threads) on the same
+// device can then never both wait on the same predecessor and run their big launches side by side.
+template <class F>
+int tcn_launch_ordered(int device, hipStream_t s, F&& launch) {
   static std::mutex mu;
   static std::unordered_map<int, hipEvent_t> last;  // device -> the last big launch's completion
   std::lock_guard<std::mutex> lk(mu);
   hipEvent_t& e = last[device];
-  if (after) {  // a fresh event per launch: a wait already enqueued never sees a later record of the same event
-    hipEvent_t n = nullptr;
-    HIPCHK(hipEventCreateWithFlags(&n, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(n, s));
-    if (e) HIPCHK(hipEventDestroy(e));  // (released once its waits have completed)
-    e = n;
-  } else if (e) {
-    HIPCHK(hipStreamWaitEvent(s, e, 0));
-  }
+  if (e) HIPCHK(hipStreamWaitEvent(s, e, 0));
+  if (const int rc = launch()) return rc;
+  // a fresh event per launch: a wait already enqueued never sees a later record of the same event
+  hipEvent_t n = nullptr;
+  HIPCHK(hipEventCreateWithFlags(&n, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(n, s));
+  if (e) HIPCHK(hipEventDestroy(e));  // (released once its waits have completed)
+  e = n;
   return SEPVAD_OK;
 }
 
@@ -1181,12 +1191,18 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       ta.hvny = h->P(h->vad_ny);
       ta.hvsx = h->vad_sx;
     }
-    // epochs per launch and group: 1 (XCD ids) + at most 3 per block per utterance (fused.hip), < 2^TCN_EPOCH_BITS;
-    // counted as 4 (headroom)
+    // diagnostics (SEPVAD_TCN_MAX_GROUPS): fewer groups per launch, so each loops over more utterances (tests reach
+    // the epoch budget below with small batches)
+    if (const int mg = env_int("SEPVAD_TCN_MAX_GROUPS", 0); mg > 0 && mg < ngroups) ngroups = mg;
+    // epochs per launch and group (fused.hip): 1 (XCD ids) + per utterance 4 per block with TF-attention (P1..P4;
+    // 3 without) + 1 for the output head (P5). The tag is salt << TCN_EPOCH_BITS | epoch, so the last epoch of a
+    // launch must stay below 2^TCN_EPOCH_BITS: an epoch carried into the salt bits would repeat the next launch's tags
     // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)
-    int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / (4 * h->nblk);
+    const int ep_utt = 4 * h->nblk + 1;
+    int max_iter = ((1 << TCN_EPOCH_BITS) - 2) / ep_utt;
     if (const int mi = env_int("SEPVAD_TCN_MAX_ITER", 0)) max_iter = std::min(max_iter, mi);
     if (max_iter < 1) return fail(SEPVAD_E_ARG, "fused TCN: too many blocks");
+    if (1 + (long long)max_iter * ep_utt >= (1 << TCN_EPOCH_BITS)) return fail(SEPVAD_E_ARG, "fused TCN: epoch budget");
     const int per_launch = max_iter * ngroups;
     const char* probe_path = getenv("SEPVAD_TCN_PROBE");
     const size_t probe_n = (size_t)h->tcn_cap * h->nblk * 16 * 9;  // wave-0 region + per-wave region
@@ -1232,14 +1248,16 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
         fprintf(stderr, "sepvad: k_tcn grid=%d G=%d groups=%d B=%d capacity=%d\n", ngl * Gt, Gt, ngl, Bl, tcn_cap_of(h));
       const bool big = tcn_big(h, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
-      if (big && tcn_order_big(h->device, s, false)) return SEPVAD_E_HIP;
-      if (ev()) return SEPVAD_E_HIP;
       TailProbe thp(h, s, "tcnhead");
       ta.hprobe = u0 == 0 ? thp.buf : nullptr;
-      HIPCHK(launch_t(ta, ngl * Gt));
+      auto run = [&]() -> int {
+        if (ev()) return SEPVAD_E_HIP;
+        HIPCHK(launch_t(ta, ngl * Gt));
+        if (ev()) return SEPVAD_E_HIP;
+        return SEPVAD_OK;
+      };
+      if (const int rc = big ? tcn_launch_ordered(h->device, s, run) : run()) return rc;
       if (ta.hprobe) HIPCHK(thp.dump(ngl * Gt, 1));
-      if (ev()) return SEPVAD_E_HIP;
-      if (big && tcn_order_big(h->device, s, true)) return SEPVAD_E_HIP;
       if (tr) {
         tr->gemm_ev.push_back((int)h->ev.size() - 2);
         tr->g2_ev.push_back((int)h->ev.size() - 2);

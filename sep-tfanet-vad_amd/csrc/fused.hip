@@ -617,7 +617,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #if TCN_GNW
           if (!LG) {
             mu = sm.gmom[0]; rs = sm.gmom[1];
-          } else {  // same doubles in the same member order as member_moments_w
+          } else {  // long groups: member_sums2's fixed order (not member_moments_w's; each bitwise reproducible per G)
             const double2 acc = member_sums2(sm.gw, G, lane);
             gn_moments_f(acc.x, acc.y, a.inv_ch, 1e-8f, mu, rs);
           }

@@ -371,8 +371,10 @@ __device__ __forceinline__ double2 member_sums2(const unsigned* gw, int G, int l
   return double2{readlane_d(s, 0), readlane_d(s, 32)};
 }
 // GroupNorm {mean, rstd} from the statistic words polled by one wave: lane base + 4 mm + {0, 1, 2, 3} holds
-// member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane): the same
-// doubles, in the same order, as member_sums2 over the words in LDS.
+// member mm's {sum lo, sum hi, sumsq lo, sumsq hi}. Sums in member order, wave-uniform (readlane). This is NOT
+// member_sums2's order (strided per-lane sums, then an xor tree): the two are different fixed orders, each chosen by
+// its instantiation (groups up to FG_WAVE members here, the long-group instantiation LG there), and each is bitwise
+// reproducible for a given G.
 __device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, double inv, float eps, float& mu, float& rs) {
   double s = 0.0, ss = 0.0;
   for (int mm = 0; mm < G; ++mm) {

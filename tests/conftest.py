@@ -58,6 +58,9 @@ def check_vad_labels(vad, v_ref, band=1e-4, flips_per=1e-4, where=""):
     allowed = max(1, int(n * flips_per))
     msg = f"{where} VAD labels: {n}, within {band:g} of 0.5: {nb}, flips there: {near_flips} (allowed {allowed})"
     print(msg)
+    if os.environ.get("SEPVAD_VAD_LABEL_LOG"):  # archived per round under profiles/ (tools/gpu_round*.sh)
+        with open(os.environ["SEPVAD_VAD_LABEL_LOG"], "a") as f:
+            f.write(os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0] + ": " + msg + "\n")
     assert far_flips == 0, f"{msg}; flips outside the band: {far_flips}"
     assert near_flips <= allowed, msg
     return n, nb, near_flips

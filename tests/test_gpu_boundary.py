@@ -369,3 +369,48 @@ def test_concurrent_long_forwards_make_progress(net):
             assert torch.equal(o[k], r[k]), k
     for st in streams:
         h.release_stream(st.cuda_stream)
+
+
+def test_two_handles_concurrent_long_forwards(net, state_dicts):
+    """Two handles on one device, each forwarding B=2 x 60 s files (groups of 118 workgroups, more than half the chip)
+    from its own host thread on its own stream, at once: the big-launch order (api.hip tcn_launch_ordered) is one
+    process-wide critical section (wait on the previous big launch, launch, record), so the two launches never run side
+    by side holding partial groups. No give-up; each output equals its serial run."""
+    import threading
+    from sep_tfanet_vad_amd import synth
+    net2 = _net(config_of("with_vad"), state_dicts["with_vad"])
+    hs = [net.native_handle(DEV), net2.native_handle(DEV)]
+    xs = [torch.from_numpy(synth.make_batch(2, 960000, 620 + k)[0]).to(DEV) for k in range(2)]
+    ref = []
+    for h, x in zip(hs, xs):
+        r = h.forward(x)
+        ref.append({k: r[k].clone() for k in ("sep", "vad", "est")})
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in hs]
+    outs = [[], []]
+    go = threading.Barrier(2)
+    errs = []
+
+    def run(i):
+        try:
+            go.wait()
+            with torch.cuda.stream(streams[i]):
+                for _ in range(3):
+                    outs[i].append(hs[i].forward(xs[i]))
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for h, o, r in zip(hs, outs, ref):
+        assert h.fused_status()
+        for oo in o:
+            for k in ("sep", "vad", "est"):
+                assert torch.equal(oo[k], r[k]), k
+    for h, st in zip(hs, streams):
+        h.release_stream(st.cuda_stream)

@@ -120,6 +120,33 @@ def test_persistent_groups_cover_large_batches(nets):
     _check_schedules(net, x[sub], c, vc)
 
 
+def test_epoch_budget_small_stack(state_dicts, monkeypatch):
+    """Hand-off epochs of one launch (api.hip enqueue_chunk): 1 + per utterance 4 per block + 1 for the output head's
+    P5 round, below 2^12. A 2-block stack (layer 2, stack 1) with 8 groups per launch (SEPVAD_TCN_MAX_GROUPS) and
+    SEPVAD_TCN_MAX_ITER unset: each group takes max_iter = 4094 // 9 = 454 utterances per launch, and the batch needs a
+    second launch, whose tags the first would have repeated under the round-4 budget (4094 // 8 = 511 utterances:
+    1 + 511 * 9 > 4095). Outputs equal the multi-kernel schedule's on every utterance."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    monkeypatch.delenv("SEPVAD_TCN_MAX_ITER", raising=False)
+    cfg = dict(config_of("with_vad"), layer=2, stack=1)
+    sd = {k: torch.from_numpy(v) for k, v in synth.make_state_dict(cfg, 77).items()}
+    net = pkg.SeparationModel(**cfg)
+    net.load_state_dict(sd, strict=True)
+    net = net.eval().to(DEV)
+    net.native_precision = "f16x3"
+    B, N = 8 * 454 + 100, 2000  # T = 8: one workgroup per utterance
+    x = torch.rand(B, N, generator=torch.Generator().manual_seed(5)) * 1.8 - 0.9
+    monkeypatch.setenv("SEPVAD_TCN_MAX_GROUPS", "8")
+    sf, vf, _, used = _run(net, x.to(DEV), True)
+    assert used
+    monkeypatch.delenv("SEPVAD_TCN_MAX_GROUPS")
+    sm, vm, _, used_m = _run(net, x.to(DEV), False)
+    assert not used_m
+    assert (sf - sm).abs().max().item() <= LO8_TOL
+    assert (vf - vm).abs().max().item() <= VAD_PROB_TOL
+
+
 def test_inference_kw_on_fused(nets):
     g = load_golden("with_vad", "small")
     ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
