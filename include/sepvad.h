@@ -149,8 +149,10 @@ int32_t sepvad_set_split(sepvad_handle h, int32_t nsplit);
  * utterance); 0 = one launch per stage (4 per block). Both meet the same parity gates. */
 int32_t sepvad_set_fused(sepvad_handle h, int32_t on);
 /* Synchronises the device and reports the schedule of the last forward and the persistent launch's
- * health: *used = 1 if it ran fused; returns SEPVAD_OK, or SEPVAD_E_HIP if a group hand-off gave up
- * (a bounded wait timed out; outputs of that forward are invalid). */
+ * health: *used = 0 if it ran one launch per stage, else the 32-frame slices per workgroup of its persistent launch
+ * (1, or 2 when the batch needs more than one round of one-slice workgroups; both give the same bits); returns
+ * SEPVAD_OK, or SEPVAD_E_HIP if a group hand-off gave up (a bounded wait timed out; outputs of that forward are
+ * invalid). */
 int32_t sepvad_fused_status(sepvad_handle h, int32_t* used);
 
 /* The side attributes of the LAST forward on `stream` (self.spectrum, self.masks_b, self.mask_per_speaker,

@@ -106,7 +106,7 @@ constexpr int TCLK_RECS = 4096;  // SEPVAD_TCN_CLOCK records kept (ring)
 struct StreamCtx {
   void* stream = nullptr;
   Workspace ws;
-  unsigned long long* tgran = nullptr;  // hand-off words [tcn_cap][2][NGR]
+  unsigned long long* tgran = nullptr;  // hand-off words [gran_slots][2][NGR]
   unsigned* terr = nullptr;             // device word: tag0 of the last launch whose hand-off wait gave up
   unsigned* herr = nullptr;             // host-mapped copy (pinned, written by the kernel)
   unsigned* herr_dev = nullptr;         // its device address
@@ -159,11 +159,15 @@ struct sepvad_model {
   __half* twq[3] = {};          // [nblk][WQ_BLOCK] fragment-ordered fp16 hi + byte lo weights: [1] e4m3, [2] int8
   int lo8 = 2;                  // k_tcn's weight lo plane: 0 fp16, 1 e4m3, 2 int8 (default); SEPVAD_WLO / sepvad_set_weight_lo
   int tcn_cap_q[3] = {};        // co-resident capacity of the byte-lo k_tcn variants
+  int tcn2_cap_p[4] = {};       // ... of the two-slice (64-frame) k_tcn, per precision
+  int tcn2_cap_q[3] = {};       // ... and per byte-lo variant
+  int gran_slots = 0;           // member slot pairs of a context's hand-off words: max(capacity, 2 x two-slice capacity)
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
+  int last_nsl = 1;             // 32-frame slices per k_tcn workgroup of the last fused forward (1 or 2)
   float* tdump = nullptr;       // parity probe buffer of the fused TCN (sepvad_set_tcn_dump), caller-owned
   // caller-stream contexts (workspace, hand-off words, give-up words); `mu` serialises the host-side
   // enqueue of concurrent callers (the kernels of different streams still overlap on the device)
@@ -476,14 +480,20 @@ int init_fused(sepvad_model* h, const Packer& pk) {
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
   for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
     // co-resident workgroups of the persistent TCN kernel that will run (both use one 512-thread workgroup per CU)
-    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, false);
+    h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, 0, 1);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
+    h->tcn2_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, 0, 2);
   }
   for (int q = 1; q <= 2; ++q) {
-    h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q);
+    h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q, 1);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_q[q]);
+    h->tcn2_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q, 2);
   }
   if (h->tcn_cap < 1) { h->fused = false; return SEPVAD_OK; }
+  // hand-off slots are per member: a two-slice workgroup publishes two members' words
+  h->gran_slots = h->tcn_cap;
+  for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) h->gran_slots = std::max(h->gran_slots, 2 * h->tcn2_cap_p[p]);
+  for (int q = 1; q <= 2; ++q) h->gran_slots = std::max(h->gran_slots, 2 * h->tcn2_cap_q[q]);
   std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
@@ -574,7 +584,7 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
   c->stream = stream;
   HIPCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   if (h->tcn_cap > 0) {
-    const size_t gb = (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long);
+    const size_t gb = (size_t)h->gran_slots * 2 * NGR * sizeof(unsigned long long);
     HIPCHK(hipMalloc(&c->tgran, gb));
     HIPCHK(hipMemsetAsync(c->tgran, 0, gb, (hipStream_t)stream));  // (ordered before this stream's first launch)
   }
@@ -609,7 +619,7 @@ int salt_reserve(sepvad_model* h, StreamCtx* c, hipStream_t s, unsigned n, unsig
     HIPCHK(hipStreamSynchronize(s));
     const unsigned v = __atomic_load_n(c->herr, __ATOMIC_ACQUIRE);
     if (v != 0 && v != c->reported) c->pending = v;
-    HIPCHK(hipMemsetAsync(c->tgran, 0, (size_t)h->tcn_cap * 2 * NGR * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(c->tgran, 0, (size_t)h->gran_slots * 2 * NGR * sizeof(unsigned long long), s));
     HIPCHK(hipMemsetAsync(c->terr, 0, 16, s));
     __atomic_store_n(c->herr, 0u, __ATOMIC_RELEASE);
     c->reported = 0;
@@ -1028,7 +1038,21 @@ int env_int(const char* name, int dflt) {
 // utterances) are therefore ordered across streams, process-wide per device: each waits on the previous one's
 // completion event (stream-ordered, no host sync). Launches of small groups need no ordering: any resident prefix
 // of 8 G workgroups completes them, beside a big launch too, and they free their CUs.
-bool tcn_big(const sepvad_model* h, int G) { return 8 * G > tcn_cap_of(h) / 2; }
+int tcn2_cap_of(const sepvad_model* h) {
+  return h->prec == PREC_F16X3 && h->lo8 ? h->tcn2_cap_q[h->lo8] : h->tcn2_cap_p[h->prec];
+}
+// Slices (32-frame members) per k_tcn workgroup for a batch of B utterances of G members: two (64 frames, fused.hip
+// TcnSmem2) once one-slice workgroups would need more than one round of the chip (B * G > capacity), so every weight
+// fragment a CU streams feeds 64 frames instead of 32; the two give the same bits, so the choice never changes a
+// result. SEPVAD_TCN_SLICES = 1 | 2 forces one (2 where the two-slice kernel applies: G even, G <= FG_WAVE).
+int tcn_slices(const sepvad_model* h, int B, int G) {
+  const int cap2 = tcn2_cap_of(h);
+  if (G % 2 || G > FG_WAVE || cap2 < G / 2) return 1;
+  if (const int f = env_int("SEPVAD_TCN_SLICES", 0)) return f == 2 ? 2 : 1;
+  const int per_round = std::max(1, tcn_cap_of(h) / G);  // utterances in one round of one-slice groups
+  return B > per_round ? 2 : 1;
+}
+bool tcn_big(int cap, int gw) { return 8 * gw > cap / 2; }
 // Runs `launch` (which enqueues one big k_tcn launch on s) behind the previous big launch of the device and records
 // its completion as the next one's wait, all under one process-wide lock: two handles (or two threads) on the same
 // device can then never both wait on the same predecessor and run their big launches side by side.
@@ -1157,10 +1181,13 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   // the VAD conv1_1 as the output head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
   const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
-    // persistent launches of the whole TCN (fused.hip), then the head GEMM on their output
-    const int Gt = G;  // workgroups per utterance
+    // persistent launches of the whole TCN (fused.hip), the output head inside them
+    const int nsl = h->tdump ? 1 : tcn_slices(h, B, G);  // (the parity-dump instantiation is one-slice only)
+    const int cap = nsl == 2 ? tcn2_cap_of(h) : tcn_cap_of(h);
+    h->last_nsl = nsl;
+    const int Gt = G / nsl;  // workgroups per utterance
     TcnArgs ta{};
-    ta.T = T; ta.Tp = Tp; ta.G = Gt; ta.nblk = h->nblk; ta.layer = c.layer;
+    ta.T = T; ta.Tp = Tp; ta.G = G; ta.nsl = nsl; ta.nblk = h->nblk; ta.layer = c.layer;
     if (const int nb = env_int("SEPVAD_TCN_NBLK", 0); nb > 0 && nb < h->nblk) ta.nblk = nb;  // diagnostics: truncated stack
     ta.ln_mode = c.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE : (c.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
     ta.tf_att = c.tf_attention;
@@ -1178,7 +1205,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     ta.dbg_delay = (unsigned)std::max(0, env_int("SEPVAD_TCN_DELAY", 0));
     ta.dump_blk = std::max(0, std::min(h->nblk - 1, env_int("SEPVAD_TCN_DUMP_BLOCK", 0)));
-    int ngroups = std::min(B, tcn_cap_of(h) / Gt);
+    int ngroups = std::min(B, cap / Gt);
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // the output head, inside k_tcn after each utterance's last block (its lo plane in the blocks' format)
     ta.hg = h->P(h->out_g); ta.hbe = h->P(h->out_b); ta.hsx = h->out_sx;
@@ -1246,8 +1273,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         HIPCHK(hipMemsetAsync(ta.clk, 0, 8 * sizeof(unsigned long long), s));
       }
       if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
-        fprintf(stderr, "sepvad: k_tcn grid=%d G=%d groups=%d B=%d capacity=%d\n", ngl * Gt, Gt, ngl, Bl, tcn_cap_of(h));
-      const bool big = tcn_big(h, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
+        fprintf(stderr, "sepvad: k_tcn grid=%d G=%d slices=%d groups=%d B=%d capacity=%d\n", ngl * Gt, G, nsl, ngl, Bl,
+                cap);
+      const bool big = tcn_big(cap, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
       TailProbe thp(h, s, "tcnhead");
       ta.hprobe = u0 == 0 ? thp.buf : nullptr;
       auto run = [&]() -> int {
@@ -1574,7 +1602,7 @@ int32_t sepvad_fused_status(sepvad_handle h, int32_t* used) {
   if (!h) return fail(SEPVAD_E_ARG, "null handle");
   DeviceGuard dg(h->device);
   std::lock_guard<std::mutex> lk(h->mu);
-  if (used) *used = h->last_fused ? 1 : 0;
+  if (used) *used = h->last_fused ? h->last_nsl : 0;
   HIPCHK(hipDeviceSynchronize());
   int rc = SEPVAD_OK;
   for (auto& c : h->ctx) {

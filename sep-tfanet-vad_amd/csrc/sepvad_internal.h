@@ -314,13 +314,14 @@ constexpr size_t WQ_W1L = 65536, WQ_W2H = 98304, WQ_W2L = 229376, WQ_BLOCK = 294
 constexpr int WQ_LO_SHIFT = 19;
 struct TcnArgs {
   int B, T, Tp, G, nblk, layer, ln_mode, tf_att, prec;
+  int nsl;               // 32-frame slices (members) per workgroup: 1, or 2 (64 frames, G even and <= FG_WAVE)
   int lo8;               // F16X3 weight lo plane: 0 fp16 (WF_* layout), 1 e4m3, 2 int8 (WQ_* layout)
   const __half* wfrag;   // [nblk][WF_BLOCK | WQ_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
   const float* prm;      // [nblk][PB_SIZE] parameter blobs
   const float* S0;       // [B][Tp][CH] TCN input (gated spectrum bins 1..256)
   GnSrc ln;              // TCN.LN statistics records (k_gate) + affine
   float alpha_h;         // TCN.output.0 PReLU
-  unsigned long long* gran;  // hand-off words [grid][2][NGR]
+  unsigned long long* gran;  // hand-off words [grid * nsl][2][NGR] (one slot pair per member)
   unsigned tag0;         // launch salt << TCN_EPOCH_BITS (tags of this launch: tag0 + epoch, epoch >= 1)
   unsigned* err;         // device word: tag0 of the last launch on this stream context whose hand-off wait gave up
   unsigned* herr;        // host-mapped (pinned) copy of the same word, read by the host without a sync
@@ -353,7 +354,7 @@ struct TcnArgs {
   unsigned long long* hprobe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [grid][8] fused-head phase stamps
 };
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s);
-int tcn_blocks_per_cu(int ln_mode, int prec, int lo);
+int tcn_blocks_per_cu(int ln_mode, int prec, int lo, int nsl = 1);
 // host: float -> e4m3fn (OCP FP8, bias 7, max 448, no inf), round to nearest even, saturating
 uint8_t e4m3_rn(float x);
 

@@ -258,6 +258,13 @@ class Handle:
         _check(self._lib.sepvad_fused_status(self._h, ctypes.byref(used)), "sepvad_fused_status")
         return bool(used.value)
 
+    def fused_slices(self) -> int:
+        """Synchronise; the 32-frame slices per workgroup of the last forward's fused TCN (1 or 2; 0 = not fused).
+        Raises if its hand-offs gave up."""
+        used = ctypes.c_int32(0)
+        _check(self._lib.sepvad_fused_status(self._h, ctypes.byref(used)), "sepvad_fused_status")
+        return int(used.value)
+
     def set_timing(self, on: bool):
         _check(self._lib.sepvad_set_timing(self._h, int(on)), "sepvad_set_timing")
 

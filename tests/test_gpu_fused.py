@@ -147,6 +147,73 @@ def test_epoch_budget_small_stack(state_dicts, monkeypatch):
     assert (vf - vm).abs().max().item() <= VAD_PROB_TOL
 
 
+def _run_slices(net, x, slices, monkeypatch, prec="f16x3"):
+    """One forward with the fused TCN forced to `slices` 32-frame slices per workgroup (SEPVAD_TCN_SLICES)."""
+    monkeypatch.setenv("SEPVAD_TCN_SLICES", str(slices))
+    net.native_precision = prec
+    h = net.native_handle(DEV)
+    try:
+        with torch.no_grad():
+            sep, vad, est = net(x)
+        used = h.fused_slices()
+    finally:
+        monkeypatch.delenv("SEPVAD_TCN_SLICES")
+        net.native_precision = "f16x3"
+    return sep, vad, est, used
+
+
+@pytest.mark.parametrize("cname", CONFIGS)
+@pytest.mark.parametrize("N", [12345, 32000, 48000, 64000, 96000, 130816])
+def test_two_slices_bitwise_equal_one_slice(cname, N, nets, monkeypatch):
+    """Two-slice workgroups (fused.hip NSL = 2: 64 frames, one weight stream for both 32-frame tiles, the depthwise conv
+    and res_out GEMM in two K halves) against one-slice workgroups: every member statistic is reduced in the one-slice
+    order, so sep, vad and est are bitwise equal. G = 2, 4, 6, 8, 12, 16 members (T = 49 .. 512), both LN modes
+    (recursive: config_with_vad, residual: config_without_vad)."""
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(3, N, 900 + N)[0]).to(DEV)
+    s1, v1, e1, u1 = _run_slices(nets[cname], x, 1, monkeypatch)
+    s2, v2, e2, u2 = _run_slices(nets[cname], x, 2, monkeypatch)
+    assert (u1, u2) == (1, 2)
+    assert torch.equal(s1, s2) and torch.equal(v1, v2) and torch.equal(e1, e2)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "f16"])
+def test_two_slices_reduced_precision_arms(prec, nets, monkeypatch):
+    """The single-product arms (BASELINE cfg 2 bf16, cfg 5 fp16) on two-slice workgroups: bitwise the one-slice
+    kernel's outputs."""
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(4, 32000, 77)[0]).to(DEV)
+    net = nets["with_vad"]
+    s1, v1, _, u1 = _run_slices(net, x, 1, monkeypatch, prec)
+    s2, v2, _, u2 = _run_slices(net, x, 2, monkeypatch, prec)
+    assert (u1, u2) == (1, 2)
+    assert torch.equal(s1, s2) and torch.equal(v1, v2)
+
+
+def test_two_slices_chosen_past_one_round_and_repeatable(nets):
+    """The launch takes two-slice workgroups once one-slice groups need more than one round of the chip (B = 128 at
+    T = 126: 512 members on 256 CUs), one-slice below; the two-slice results are bitwise repeatable run to run and
+    equal the one-slice results of the same utterances in a small batch (batch invariance across the two kernels)."""
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(128, 32000, 4343)[0]).to(DEV)
+    outs = []
+    for _ in range(3):
+        with torch.no_grad():
+            outs.append(net(x))
+        assert h.fused_slices() == 2
+    for o in outs[1:]:
+        for a_, b_ in zip(outs[0], o):
+            assert torch.equal(a_, b_)
+    sub = [0, 1, 63, 64, 127]
+    with torch.no_grad():
+        small = net(x[sub])
+    assert h.fused_slices() == 1
+    for a_, b_ in zip(outs[0], small):
+        assert torch.equal(a_[sub], b_)
+
+
 def test_inference_kw_on_fused(nets):
     g = load_golden("with_vad", "small")
     ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
