@@ -65,7 +65,9 @@ def tcn_flops(B, T, precision="f16x3", nblk=24):
 
 def weight_bytes(precision, wlo="f16"):
     """Bytes per pointwise weight streamed by the fused TCN: fp16 hi + fp16 lo (f16x3), fp16 hi + a byte lo plane
-    (f16x3 with --wlo e4m3 / i8), or one 16-bit plane (f16 / bf16)."""
+    (f16x3 with --wlo e4m3 / i8), one 16-bit plane (f16 / bf16) or fp32."""
+    if precision == "fp32":
+        return 4
     return (4 if wlo == "f16" else 3) if precision == "f16x3" else 2
 
 
@@ -152,7 +154,7 @@ def res_out_bytes(B, T):
 
 
 STATS_FILE = "r04prof_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
-TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false, false>"  # the dominant kernel's name in that file
+TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false, false, 1>"  # the dominant kernel's name in that file
 
 
 def rocprof_avg_us(kernel_prefix):
@@ -462,6 +464,9 @@ def main():
             if args.precision == "f16x3":
                 peak = F16_MFMA_PEAK_TFLOPS / 3.0
                 kern = body + "fp16x3 split on v_mfma_f32_32x32x16_f16: peak = 2.5 PF/s / 3)"
+            elif args.precision == "fp32":
+                peak = FP32_MFMA_PEAK_TFLOPS
+                kern = body + "exact fp32 on v_mfma_f32_32x32x2_f32, fp32 weights streamed: peak = 157.3 TF/s)"
             else:
                 peak = F16_MFMA_PEAK_TFLOPS
                 kern = body + f"{args.precision} operands on v_mfma_f32_32x32x16_{args.precision}: peak = 2.5 PF/s)"

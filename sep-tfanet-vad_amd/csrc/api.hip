@@ -51,6 +51,7 @@ struct PackedW {
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
   size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
   size_t fi8 = 0;           // ... the same as int8 steps of 2^-WQ_LO_SHIFT, biased by 128
+  size_t ff32 = 0;          // the row-scaled fp32 weight in the same fragment order (float blob; fused PREC_F32)
 };
 
 struct BlockOff {
@@ -164,6 +165,7 @@ struct sepvad_model {
   int gran_slots = 0;           // member slot pairs of a context's hand-off words: max(capacity, 2 x two-slice capacity)
   __half* twf16 = nullptr;      // [nblk][WS_BLOCK] fragment-ordered fp16 weights (F16)
   __half* twbf = nullptr;       // [nblk][WS_BLOCK] fragment-ordered bf16 bits (BF16)
+  float* twf32 = nullptr;       // [nblk][WS32_BLOCK / 2] fragment-ordered fp32 weights (F32)
   float* tprm = nullptr;        // [nblk][PB_SIZE] parameter blobs
   bool last_fused = false;
   float out_sx = 1.f;           // fp16 range scale of the head GEMM's A operand (undone by wout.scale)
@@ -283,6 +285,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
   std::vector<__half> hi((size_t)mpad * cin), lo((size_t)mpad * cin), bf((size_t)mpad * cin);
   std::vector<float> lo32((size_t)mpad * cin);  // the exact fp32 residual (source of the e4m3 lo plane)
+  std::vector<float> srow(mpad, 1.f);           // the row scale 2^-e
   for (int o = 0; o < mpad; ++o) {
     float mx = 0.f;
     if (o < cout)
@@ -290,6 +293,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
     int e = 0;
     if (mx > 0.f) { (void)std::frexp(mx, &e); }  // mx = f * 2^e, f in [0.5, 1)
     const float s = std::ldexp(1.f, -e);
+    srow[o] = s;
     sc[o] = std::ldexp(1.f, e + col_e);
     for (int i = 0; i < cin; ++i) {
       const float v = o < cout ? w[(size_t)o * cin + i] : 0.f;
@@ -312,6 +316,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   // k = 16*s + 8*(l >> 5) + j.
   if (mpad % 32 == 0 && cin % 16 == 0) {
     std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin), fb((size_t)mpad * cin);
+    std::vector<float> ff((size_t)mpad * cin);
     size_t q = 0;
     for (int mt = 0; mt < mpad / 32; ++mt)
       for (int st = 0; st < cin / 16; ++st)
@@ -321,7 +326,10 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
             fh[q] = hi[src];
             fl[q] = lo[src];
             fb[q] = bf[src];
+            // exact: a power-of-two row scale (PREC_F32: v_mfma_f32_32x32x2_f32 pairs k = 8 h + j, fused.hip)
+            ff[q] = w32[src] * srow[src / cin];
           }
+    p.ff32 = pk.add(ff);
     p.fhi = pk.addh(fh);
     p.flo = pk.addh(fl);
     p.fbf = pk.addh(fb);
@@ -478,11 +486,11 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int ln = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE ? LD_RECURSIVE
                  : (h->cfg.ln_mode == SEPVAD_LN_RESIDUAL ? LD_RESIDUAL : LD_ADD);
-  for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) {
+  for (int p : {PREC_F16X3, PREC_F16, PREC_BF16, PREC_F32}) {
     // co-resident workgroups of the persistent TCN kernel that will run (both use one 512-thread workgroup per CU)
     h->tcn_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, 0, 1);
     h->tcn_cap = std::max(h->tcn_cap, h->tcn_cap_p[p]);
-    h->tcn2_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, 0, 2);
+    h->tcn2_cap_p[p] = ncu * tcn_blocks_per_cu(ln, p, 0, 2);  // (0 for PREC_F32: one-slice only)
   }
   for (int q = 1; q <= 2; ++q) {
     h->tcn_cap_q[q] = ncu * tcn_blocks_per_cu(ln, PREC_F16X3, q, 1);
@@ -496,6 +504,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   for (int q = 1; q <= 2; ++q) h->gran_slots = std::max(h->gran_slots, 2 * h->tcn2_cap_q[q]);
   std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
+  std::vector<float> wf32(WS32_BLOCK / 2 * h->nblk);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
   for (int i = 0; i < h->nblk; ++i) {
     const BlockOff& bo = h->blk[i];
@@ -518,6 +527,9 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WS_BLOCK - WS_W2, ws16.data() + WS_BLOCK * i + WS_W2);
     std::copy_n(pk.hblob.begin() + bo.w1.fbf, WS_W2, wsbf.data() + WS_BLOCK * i);
     std::copy_n(pk.hblob.begin() + bo.w2.fbf, WS_BLOCK - WS_W2, wsbf.data() + WS_BLOCK * i + WS_W2);
+    float* f32b = wf32.data() + WS32_BLOCK / 2 * i;
+    std::copy_n(pk.blob.begin() + bo.w1.ff32, WS32_W2 / 2, f32b);
+    std::copy_n(pk.blob.begin() + bo.w2.ff32, (WS32_BLOCK - WS32_W2) / 2, f32b + WS32_W2 / 2);
     float* q = pb.data() + (size_t)PB_SIZE * i;
     auto put = [&](int off, size_t src, int n) { std::copy_n(pk.blob.begin() + src, n, q + off); };
     put(PB_WS1, bo.w1.scale, CH); put(PB_B1, bo.b1, CH); put(PB_G1, bo.g1, CH); put(PB_BE1, bo.be1, CH);
@@ -548,6 +560,8 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   HIPCHK(hipMemcpy(h->twq[2], wi.data(), wi.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twf16, ws16.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf16, ws16.data(), ws16.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twf32, wf32.size() * sizeof(float)));
+  HIPCHK(hipMemcpy(h->twf32, wf32.data(), wf32.size() * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twbf, wsbf.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twbf, wsbf.data(), wsbf.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->tprm, pb.size() * sizeof(float)));
@@ -1023,7 +1037,7 @@ int tcn_cap_of(const sepvad_model* h) {
 
 bool fused_ok(const sepvad_model* h, int T) {
   const int G = (T + FR - 1) / FR;
-  return h->fused && h->prec != PREC_F32 && G <= FG_MAX && tcn_cap_of(h) >= G;
+  return h->fused && G <= FG_MAX && tcn_cap_of(h) >= G;
 }
 
 int env_int(const char* name, int dflt) {
@@ -1193,7 +1207,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.tf_att = c.tf_attention;
     ta.prec = h->prec;
     ta.lo8 = h->prec == PREC_F16X3 ? h->lo8 : 0;
-    ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq[ta.lo8] : h->twf) : (h->prec == PREC_F16 ? h->twf16 : h->twbf);
+    ta.wfrag = h->prec == PREC_F16X3 ? (ta.lo8 ? h->twq[ta.lo8] : h->twf)
+                                     : (h->prec == PREC_F16 ? h->twf16
+                                                            : (h->prec == PREC_F32 ? reinterpret_cast<const __half*>(h->twf32) : h->twbf));
     ta.prm = h->tprm;
     ta.inv_ch = 1.0 / ((double)CH * T);
     ta.inv_hid = 1.0 / ((double)HID * T);
@@ -1209,12 +1225,14 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     if (ngroups >= 8) ngroups -= ngroups % 8;
     // the output head, inside k_tcn after each utterance's last block (its lo plane in the blocks' format)
     ta.hg = h->P(h->out_g); ta.hbe = h->P(h->out_b); ta.hsx = h->out_sx;
-    ta.hwh = h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
+    ta.hwh = h->prec == PREC_F32 ? reinterpret_cast<const __half*>(h->P(h->wout_spk.ff32))
+                                 : h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
     ta.hwl = h->H(ta.lo8 == 2 ? h->wout_spk.fi8 : (ta.lo8 == 1 ? h->wout_spk.fl8 : h->wout_spk.flo));
     ta.hwscale = h->P(h->wout_spk.scale); ta.hbias = h->P(h->bo_spk);
     ta.hnyw = h->P(h->out_nyw); ta.hnyb = h->P(h->out_nyb);
     if (vad_in_head) {
       ta.hvwh = h->H(h->vadw.fhi); ta.hvwl = h->H(h->vadw.flo); ta.hvwscale = h->P(h->vadw.scale);
+      ta.hvwf = h->P(h->vadw.ff32);
       ta.hvny = h->P(h->vad_ny);
       ta.hvsx = h->vad_sx;
     }
@@ -1916,6 +1934,7 @@ void sepvad_destroy(sepvad_handle h) {
     if (q) (void)hipFree(q);
   if (h->twf16) (void)hipFree(h->twf16);
   if (h->twbf) (void)hipFree(h->twbf);
+  if (h->twf32) (void)hipFree(h->twf32);
   if (h->tprm) (void)hipFree(h->tprm);
   if (h->tprobe) (void)hipFree(h->tprobe);
   if (h->tclk) (void)hipFree(h->tclk);

@@ -60,6 +60,10 @@ constexpr int NTHR = 512;         // 8 waves; wave w owns output channels [32w, 
 constexpr int LDX = CH + 8;       // x' row stride (halves): 132 dwords == 4 (mod 64) => conflict-free b128 reads
 constexpr int LDD = HID + 8;      // d row stride (halves): 260 dwords == 4 (mod 64)
 constexpr int HROW = FR + 8;      // conv1d output rows incl. 4 halo rows on each side
+// PREC_F32 (exact fp32 GEMMs on v_mfma_f32_32x32x2_f32): the A operands are single fp32 planes in the same LDS, x'
+// [32][LDXF] (= the hi plane's bytes) and d [32][LDDF] (within hi + lo), row strides == 4 (mod 64) dwords as above
+constexpr int LDXF = CH + 4;
+constexpr int LDDF = HID + 4;
 #ifndef TCN_PD
 #define TCN_PD 8     // weight K steps in flight per wave (4: +10 us; 16: spills at 2 waves per SIMD)
 #endif
@@ -148,14 +152,17 @@ template <int NSL> struct SmemOf { using type = TcnSmem; };
 template <> struct SmemOf<2> { using type = TcnSmem2; };
 
 // Weight-blob layout per operand format (api.hip init_fused): fp16x3 hi/lo planes, or one plane.
+// PREC_F32: one fp32 plane per GEMM (WS32_*, in __half units of the blob pointer), 2 KB per wave per K step.
 template <int PRE, int LQ = 0>
 struct WLay {
   static constexpr bool L8 = LQ != 0;
   static constexpr bool X3 = PRE == PREC_F16X3;
-  static constexpr size_t BLOCK = X3 ? (L8 ? WQ_BLOCK : WF_BLOCK) : WS_BLOCK;
+  static constexpr bool F32 = PRE == PREC_F32;
+  static constexpr size_t BLOCK = X3 ? (L8 ? WQ_BLOCK : WF_BLOCK) : (F32 ? WS32_BLOCK : WS_BLOCK);
   static constexpr size_t W1H = 0, W1L = X3 ? (L8 ? WQ_W1L : WF_W1L) : 0;
-  static constexpr size_t W2H = X3 ? (L8 ? WQ_W2H : WF_W2H) : WS_W2, W2L = X3 ? (L8 ? WQ_W2L : WF_W2L) : 0;
+  static constexpr size_t W2H = X3 ? (L8 ? WQ_W2H : WF_W2H) : (F32 ? WS32_W2 : WS_W2), W2L = X3 ? (L8 ? WQ_W2L : WF_W2L) : W2H;
 };
+template <int PRE> constexpr int wstep_bytes() { return PRE == PREC_F32 ? 2048 : 1024; }  // per wave per K step
 
 // conv1d / res_out GEMM of one wave: acc[t][32 frames x 32 channels] += A[32 t .. 32 t + 31][16*NS] * W^T for the NT
 // 32-frame tiles of the workgroup (each weight fragment feeds all NT tiles). A comes from LDS (hi/lo planes, row stride
@@ -165,11 +172,67 @@ struct WLay {
 // PRE: PREC_F16X3 = 3 fp16 products per step (hi/lo planes); PREC_F16 / PREC_BF16 = 1 product on the
 // hi plane (fp16 or bf16 bits), no lo plane, half the weight stream.
 
+// PREC_F32: eight v_mfma_f32_32x32x2_f32 per 16-deep step, MFMA j on the K pair (j, 8 + j) of the step (lane half h
+// carries k = 8 h + j: the A reads are 8 consecutive floats per lane, the same element order as the fp16 fragments);
+// the lane's 8 weight floats of a step are ring entries rh (0..3) and rl (4..7), loaded at voff and voffl = voff + 16.
+template <int NS, int LDA, int RD, int NT, int KS0>
+__device__ __forceinline__ void wave_gemm_f32(f32x16v (&acc)[NT], const float* Af, __amdgpu_buffer_rsrc_t wh,
+                                              int voff, int voffl, u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
+  constexpr int SB = wstep_bytes<PREC_F32>();
+  const int aoff = (lane & 31) * LDA + 8 * (lane >> 5);
+  f32x4 a0[2][NT], a1[2][NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    a0[0][t] = *reinterpret_cast<const f32x4*>(Af + aoff + t * FR * LDA);
+    a1[0][t] = *reinterpret_cast<const f32x4*>(Af + aoff + t * FR * LDA + 4);
+  }
+  auto step = [&](int s, int i, bool pf) {
+    const int cur = s & 1, nxt = cur ^ 1;
+    if (s + 1 < NS) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        a0[nxt][t] = *reinterpret_cast<const f32x4*>(Af + aoff + t * FR * LDA + 16 * (s + 1));
+        a1[nxt][t] = *reinterpret_cast<const f32x4*>(Af + aoff + t * FR * LDA + 16 * (s + 1) + 4);
+      }
+    }
+    // (whole ring entries bit-cast: this hipcc's __builtin_bit_cast(float, v[j]) on a vector element reads element 0
+    // for every j -- seen in the ISA as one B register for all four MFMAs)
+    const f32x4 bh = __builtin_bit_cast(f32x4, rh[i]), bl = __builtin_bit_cast(f32x4, rl[i]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[cur][t][j], bh[j], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[cur][t][j], bl[j], acc[t], 0, 0, 0);
+    }
+    if (pf) {
+      rh[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (KS0 + s + RD) * SB, 0);
+      rl[i] = __builtin_amdgcn_raw_buffer_load_b128(wh, voffl, (KS0 + s + RD) * SB, 0);
+    }
+    if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NT, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8 * NT, 0);
+    if (pf) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll
+  for (int s0 = 0; s0 < NS - RD; s0 += RD) {
+#pragma unroll
+    for (int i = 0; i < RD; ++i) step(s0 + i, i, true);
+  }
+#pragma unroll
+  for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
+}
+
 template <int NS, int LDA, int PRE, int RD = PD, int LQ = 0, int NT = 1, int KS0 = 0>
 __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
   static_assert(NS % RD == 0 && NS >= RD && KS0 % RD == 0, "K steps");
+  if constexpr (PRE == PREC_F32) {
+    (void)Alo; (void)wl;
+    wave_gemm_f32<NS, LDA, RD, NT, KS0>(acc, reinterpret_cast<const float*>(Ahi), wh, voff, voffl, rh, rl, lane);
+    return;
+  } else {
   constexpr bool L8 = LQ != 0;
   static_assert(!L8 || (PRE == PREC_F16X3 && RD % 2 == 0), "byte lo plane: F16X3, K-step pairs");
   constexpr bool X3 = PRE == PREC_F16X3;
@@ -249,6 +312,7 @@ __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ah
   }
 #pragma unroll
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
+  }
 }
 
 template <int PRE, int RD = PD, int LQ = 0>
@@ -257,8 +321,10 @@ __device__ __forceinline__ void prefetch_w(__amdgpu_buffer_rsrc_t wh, __amdgpu_b
   constexpr bool L8 = LQ != 0;
 #pragma unroll
   for (int s = 0; s < RD; ++s) {
-    rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * 1024, 0);
-    if constexpr (L8) {
+    rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, s * wstep_bytes<PRE>(), 0);
+    if constexpr (PRE == PREC_F32) {
+      rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voffl, s * wstep_bytes<PRE>(), 0);
+    } else if constexpr (L8) {
       if (s % 2 == 0) rl[s / 2] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, (s / 2) * 1024, 0);
     } else if constexpr (PRE == PREC_F16X3) {
       rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, s * 1024, 0);
@@ -272,19 +338,43 @@ template <int PRE, int RD, int LQ = 0>
 __device__ __forceinline__ void prefetch_w1(__amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                             u32x4v (&rh)[RD], u32x4v (&rl)[RD], int s, int sb = 0) {
   constexpr bool L8 = LQ != 0;
-  rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (sb + s) * 1024, 0);
-  if constexpr (L8) {
+  rh[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voff, (sb + s) * wstep_bytes<PRE>(), 0);
+  if constexpr (PRE == PREC_F32) {
+    rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wh, voffl, (sb + s) * wstep_bytes<PRE>(), 0);
+  } else if constexpr (L8) {
     if (s % 2 == 0) rl[s / 2] = __builtin_amdgcn_raw_buffer_load_b128(wl, voffl, ((sb + s) / 2) * 1024, 0);
   } else if constexpr (PRE == PREC_F16X3) {
     rl[s] = __builtin_amdgcn_raw_buffer_load_b128(wl, voff, (sb + s) * 1024, 0);
   }
 }
 
+// store_d4 (tcn_common.h) at element idx of the planes; PREC_F32: hidden 2c..2c+3 as one 16-byte store of 4 floats
+template <int PRE>
+__device__ __forceinline__ void store_d4i(_Float16* hi, _Float16* lo, int idx, f32x2 y0, f32x2 y1) {
+  if constexpr (PRE == PREC_F32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(hi) + idx) = f32x4{y0.x, y1.x, y0.y, y1.y};
+  } else {
+    store_d4<PRE>(hi + idx, lo + idx, y0, y1);
+  }
+}
+// element e of an A plane as a plane pointer (fp32 planes count floats)
+template <int PRE>
+__device__ __forceinline__ _Float16* plane_at(_Float16* p, int e) {
+  if constexpr (PRE == PREC_F32) return reinterpret_cast<_Float16*>(reinterpret_cast<float*>(p) + e);
+  else return p + e;
+}
+
 // diagnostics (SEPVAD_TCN_PROBE): wave 0's wall clock at 13 phase points of every block of the first
 // utterance each workgroup processes: probe[(blockIdx * nblk + block) * 16 + point]; and every wave's at the
 // same points (lane 0 of each wave) after that region: probe[grid*nblk*16 + ((blockIdx*nblk + block)*16 + point)*8 + wave]
+#ifdef TCN_MARK  // static census builds only (tools/isa_phases.py): an assembly comment at every phase point
+#define TMARK(k) asm volatile(";;TMARK " #k)
+#else
+#define TMARK(k)
+#endif
 #define TPROBE(k)                                                                                  \
   do {                                                                                             \
+    TMARK(k);                                                                                      \
     if (TP_ON && (tid & 63) == 0 && u == grp) {                                                   \
       const unsigned long long _t = wall_clock64();                                                \
       const size_t _i = ((size_t)blockIdx.x * a.nblk + bi) * 16 + (k);                            \
@@ -328,6 +418,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // NSL: 32-frame slices (members) per workgroup. Two-slice workgroups serve short groups only (G even, <= FG_WAVE)
   static_assert(NSL == 1 || (NSL == 2 && !LG && !DUMP), "two-slice workgroups: short groups, no parity dumps");
   constexpr int FW = FR * NSL;  // frames of this workgroup
+  // PREC_F32: exact fp32 GEMMs; the A planes hold fp32 rows (strides LDXF / LDDF floats), the weight stream 2 KB per wave
+  // and K step (lane offsets voff and voff + 16)
+  constexpr bool F32 = PRE == PREC_F32;
+  static_assert(!F32 || (NSL == 1 && !DUMP), "fp32 GEMMs: one-slice workgroups");
+  constexpr int LDXE = F32 ? LDXF : LDX, LDDE = F32 ? LDDF : LDD;  // A-plane row strides in elements
+  constexpr int VB = F32 ? 32 : 16;                                // weight bytes per lane per K step
   using Smem = typename SmemOf<NSL>::type;
   // phase stamps only in the probe instantiation (SEPVAD_TCN_PROBE): none of their pointers or branches in production
   const bool TP_ON = PROBE && a.probe != nullptr;
@@ -370,6 +466,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     __hip_atomic_fetch_max(a.clk, ~rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0) { a.clk[2] = rt; a.clk[4] = __builtin_amdgcn_s_memtime(); }
   }
+  // epoch 1: this workgroup's XCD id for each of its members (write-through), polled in the first utterance's prologue
+  if (tid < NSL && grp < a.B)
+    gput(slot(m0 + tid, 1), a.tag0 + 1, __builtin_amdgcn_s_getreg(6164) & 0xfu, false);  // hwreg(HW_REG_XCC_ID, 0, 4)
   if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact (two slices: not applied)
     if (tid < CH) sm.af[tid] = 1.f;
     if (tid < FW) sm.at[tid] = 1.f;
@@ -385,9 +484,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const int T = a.T, Tp = a.Tp, t0 = g * FW;
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
-  const int voff1 = (wave * NS1 * 64 + lane) * 16, voff2 = (wave * NS2 * 64 + lane) * 16;
-  // ... and of its 16-B lo fragment pair (e4m3 lo plane: one 1 KB wave load per two K steps)
-  const int voff1l = (wave * (NS1 / 2) * 64 + lane) * 16, voff2l = (wave * (NS2 / 2) * 64 + lane) * 16;
+  const int voff1 = (wave * NS1 * 64 + lane) * VB, voff2 = (wave * NS2 * 64 + lane) * VB;
+  // ... and of its 16-B lo fragment pair (byte lo planes: one 1 KB wave load per two K steps), or (fp32) of its
+  // second 16 bytes
+  const int voff1l = F32 ? voff1 + 16 : (wave * (NS1 / 2) * 64 + lane) * 16;
+  const int voff2l = F32 ? voff2 + 16 : (wave * (NS2 / 2) * 64 + lane) * 16;
 
   for (int u = grp; u < a.B; u += ngroups) {
     // opaque per-utterance copies (as in the block loop): keeps hipcc from hoisting and spilling the
@@ -415,7 +516,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const __amdgpu_buffer_rsrc_t gr = rsrc_of(ka->ln.g), ber = rsrc_of(ka->ln.be);
       const __amdgpu_buffer_rsrc_t w1h = rsrc_of(ka->wfrag), w1l = rsrc_of(ka->wfrag + WL::W1L);
       const int vo = (hl4u * CH + m) * 4, co = (tid & (CH - 1)) * 4;
-      const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * 16, voffu_l = (wave_s * (NS1 / 2) * 64 + (tid & 63)) * 16;
+      const int voffu = (wave_s * NS1 * 64 + (tid & 63)) * VB;
+      const int voffu_l = F32 ? voffu + 16 : (wave_s * (NS1 / 2) * 64 + (tid & 63)) * 16;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 16 * NSL; ++r)  // rows < G*32 <= Tp: in bounds (masked below)
@@ -435,8 +537,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
     if (u == grp) {
       // the members' XCD ids (write-through, epoch 1); if the whole group shares one XCD, every later
       // hand-off keeps its words in that XCD's L2 (correct for any placement: checked, not assumed)
-      const unsigned xcc = __builtin_amdgcn_s_getreg(6164) & 0xfu;  // hwreg(HW_REG_XCC_ID, 0, 4)
-      if (tid < NSL) gput(slot(m0 + tid, 1), a.tag0 + 1, xcc, false);
+      // (published at kernel entry, so its round trip overlaps the input loads)
       const u64* p[1] = {tid < G ? slot(tid, 1) : nullptr};
       unsigned v[1];
       gpoll<1>(p, a.tag0 + 1, v, a);
@@ -471,7 +572,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       for (int r = 0; r < 16 * NSL; ++r) {
         const int tl = trow(r);
         o[r] = fmaf(raw[r], s, h) * (t0 + tl < T ? 1.f : 0.f);
-        split_store<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
+        split_store<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, o[r] * sx0);  // x' * 2^-e (range guard, PB_SX)
       }
       if (float* dp = DUMP ? kargs()->dump : nullptr) {  // parity probe: TCN.LN output (model/model.py:333); pointer re-read
 #pragma unroll                           // from the kernarg segment at use (no register held across the loop)
@@ -525,8 +626,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[sl][r] = 0.f;
       {
-        wave_gemm<NS1, LDX, PRE, RD, LQ, NSL>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, voff1l, rh,
-                                              rl, lane);
+        wave_gemm<NS1, LDXE, PRE, RD, LQ, NSL>(acc, sm.Ahi, sm.Alo, rsrc_of(wb), rsrc_of(wb + WL::W1L), voff1, voff1l, rh,
+                                               rl, lane);
       TPROBE(1);
       }
       {
@@ -660,7 +761,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               s0 += y[q];
               s1 = __builtin_elementwise_fma(y[q], y[q], s1);
             }
-            store_d4<PRE>(sm.Ahi + tl * LDA + 2 * c2 - acol0, sm.Alo + tl * LDA + 2 * c2 - acol0, y[0], y[1]);
+            store_d4i<PRE>(sm.Ahi, sm.Alo, tl * LDA + 2 * c2 - acol0, y[0], y[1]);
           }
         };
         static_assert(RD == RPI * FR / 4, "RPI ring entries per frame of the packed depthwise conv");
@@ -685,7 +786,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         if (TCN_SUB == 1) TPROBE(13);
         f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
         // thread = input channels c2, c2+1 (hidden 2c2..2c2+3) x frames fr0..fr0+7
-        dwconv(std::integral_constant<int, LDD>{}, 2 * (tid & (CH / 2 - 1)), (tid >> 7) * (FR / 4), 0, 0, s0, s1);
+        dwconv(std::integral_constant<int, LDDE>{}, 2 * (tid & (CH / 2 - 1)), (tid >> 7) * (FR / 4), 0, 0, s0, s1);
         float st[2] = {s0.x + s0.y, s1.x + s1.y};
         if (TCN_SUB == 1) TPROBE(14);
         block_sums<2>(st, sm.red, sm.dred, tid);  // barrier inside: d complete in LDS
@@ -698,7 +799,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[sl][r] = 0.f;
       if constexpr (NSL == 1) {
-        wave_gemm<NS2, LDD, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, voff2l, rh, rl, lane);
+        wave_gemm<NS2, LDDE, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, voff2l, rh, rl, lane);
       } else {
         // two K halves of 256 hidden channels each (input channels 0..127, then 128..255 of the depthwise conv) through
         // the same A planes. The member statistics of d: per half every wave's totals of the pass it ran, which is the
@@ -1083,7 +1184,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       const int hjl = (wave_s + (blockIdx.x >> 3)) & 7;
       const __amdgpu_buffer_rsrc_t wnh = lastb ? rsrc_of(a.hwh) : rsrc_of(wb + WL::BLOCK);
       const __amdgpu_buffer_rsrc_t wnl = lastb ? rsrc_of(PRE == PREC_F16X3 ? a.hwl : a.hwh) : rsrc_of(wb + WL::BLOCK + WL::W1L);
-      const int pvo = lastb ? (hjl * NS1 * 64 + lane) * 16 : voff1, pvol = lastb ? (hjl * (NS1 / 2) * 64 + lane) * 16 : voff1l;
+      const int pvo = lastb ? (hjl * NS1 * 64 + lane) * VB : voff1;
+      const int pvol = lastb ? (F32 ? pvo + 16 : (hjl * (NS1 / 2) * 64 + lane) * 16) : voff1l;
       if (TCN_SUB == 0) TPROBE(14);
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
@@ -1101,8 +1203,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
           const f32x2 ov = x * vm;
           o[r] = ov.x; o[r + 1] = ov.y;
-          if (TCN_XPK) split_store_rows_pk<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn, (lane & 1) != 0);
-          else split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDX + m, LDX, ov * sxn);
+          if (TCN_XPK) split_store_rows_pk<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn, (lane & 1) != 0);
+          else split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn);
         }
       }
       __syncthreads();
@@ -1174,7 +1276,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const float sc = rs * a.hg[mh], sh = a.hbe[mh] - sc * mu;
 #pragma unroll
         for (int r = 0; r < 16 * NSL; ++r)
-          split_store<PRE>(sm.Ahi, sm.Alo, trow(r) * LDX + mh, fmaf(prelu_f(o[r], a.alpha_h), sc, sh) * a.hsx);
+          split_store<PRE>(sm.Ahi, sm.Alo, trow(r) * LDXE + mh, fmaf(prelu_f(o[r], a.alpha_h), sc, sh) * a.hsx);
       }
       __syncthreads();  // A complete
       hstamp(3);
@@ -1182,8 +1284,10 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // this wave's VAD tile: [32 frames][32 channels], 16-B granules XOR-swizzled by frame: one slice, in the unused
       // tail of the A planes (row stride LDD, only LDX in use); two slices, in H past one slice's tap products. The
       // waves' tap products [8][2][FR][20] of one slice in H (free now)
-      float* const vsc = NSL == 1 ? reinterpret_cast<float*>((wave_s < 4 ? sm.Ahi : sm.Alo) + FR * LDX) + (wave_s & 3) * FR * 32
-                                  : sm.H + 16 * FR * HEAD_VAD_N + wave_s * FR * 32;
+      // (fp32: the head's A fills the hi plane's bytes, the 8 tiles go to the lo plane)
+      float* const vsc = F32 ? reinterpret_cast<float*>(sm.Alo) + wave_s * FR * 32
+                             : (NSL == 1 ? reinterpret_cast<float*>((wave_s < 4 ? sm.Ahi : sm.Alo) + FR * LDX) + (wave_s & 3) * FR * 32
+                                         : sm.H + 16 * FR * HEAD_VAD_N + wave_s * FR * 32);
       float* const Ps = sm.H;
       auto vidx = [](int t, int c) { return t * 32 + ((((c >> 2) ^ t) & 7) << 2) + (c & 3); };
       float* const nys = NSL == 1 ? &sm.c[0][0] : reinterpret_cast<float*>(sm.gw);  // [2][FR] bin 256 (free now)
@@ -1194,20 +1298,20 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // opaque per-slice lane values (as in the block loop): the per-row addresses are not hoisted across the slices
         const int tidh = fresh_tid(wave_s), lh = tidh & 63, hl4h = 4 * ((tidh >> 5) & 1);
         auto trow1 = [&](int r) { return (r & 3) + 8 * (r >> 2) + hl4h; };  // row r < 16 of one slice's tile
-        auto tile_voff = [&](int q) { return ((q * (HEAD_SPK / 32) + jl) * NS1 * 64 + lh) * 16; };
-        auto tile_voffl = [&](int q) { return ((q * (HEAD_SPK / 32) + jl) * (NS1 / 2) * 64 + lh) * 16; };
+        auto tile_voff = [&](int q) { return ((q * (HEAD_SPK / 32) + jl) * NS1 * 64 + lh) * VB; };
+        auto tile_voffl = [&](int q) { return F32 ? tile_voff(q) + 16 : ((q * (HEAD_SPK / 32) + jl) * (NS1 / 2) * 64 + lh) * 16; };
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int jt = q * (HEAD_SPK / 32) + jl;  // row tile of the weight copy
           f32x16v acc[1];
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[0][r] = 0.f;
-          wave_gemm<NS1, LDX, PRE, RD, LQ>(acc, sm.Ahi + FR * sl * LDX, sm.Alo + FR * sl * LDX, wh, wl, tile_voff(q),
-                                           tile_voffl(q), rh, rl, lh);
+          wave_gemm<NS1, LDXE, PRE, RD, LQ>(acc, plane_at<PRE>(sm.Ahi, FR * sl * LDXE), plane_at<PRE>(sm.Alo, FR * sl * LDXE),
+                                            wh, wl, tile_voff(q), tile_voffl(q), rh, rl, lh);
           if (q == 0) prefetch_w<PRE, RD, LQ>(wh, wl, tile_voff(1), tile_voffl(1), rh, rl);
           else if (sl + 1 < NSL) prefetch_w<PRE, RD, LQ>(wh, wl, tile_voff(0), tile_voffl(0), rh, rl);
           f16x8 vb[2][2];
-          if (vad) {
+          if (vad && !F32) {
 #pragma unroll
             for (int st = 0; st < 2; ++st) {
               vb[st][0] = *reinterpret_cast<const f16x8*>(a.hvwh + ((size_t)(2 * jl + st) * 64 + lh) * 8);
@@ -1234,6 +1338,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               const int tr = lh & 31, c0 = 16 * st + 8 * (lh >> 5);
               const f32x4 x0 = *reinterpret_cast<const f32x4*>(vsc + vidx(tr, c0));
               const f32x4 x1 = *reinterpret_cast<const f32x4*>(vsc + vidx(tr, c0 + 4));
+              if constexpr (F32) {  // fp32 tap products (the K-pair convention of wave_gemm_f32), weights a.hvwf
+                const float* wf = a.hvwf + ((size_t)(2 * jl + st) * 64 + lh) * 8;
+                const f32x4 b0 = *reinterpret_cast<const f32x4*>(wf), b1 = *reinterpret_cast<const f32x4*>(wf + 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pv = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[j], b0[j], pv, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) pv = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[j], b1[j], pv, 0, 0, 0);
+                continue;
+              }
               f16x8 ah, al;
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
@@ -1266,7 +1379,12 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           for (int k = 0; k < 4; ++k) {
             // (read as the type split_store wrote: bf16 planes through __bf16, fp16 through _Float16)
             float xv[8];
-            if constexpr (PRE == PREC_BF16) {
+            if constexpr (F32) {
+              const float* af = reinterpret_cast<const float*>(sm.Ahi) + (FR * sl + tn) * LDXE + 32 * part + 8 * k;
+              const f32x4 u0 = *reinterpret_cast<const f32x4*>(af), u1 = *reinterpret_cast<const f32x4*>(af + 4);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) xv[e] = e < 4 ? u0[e] : u1[e - 4];
+            } else if constexpr (PRE == PREC_BF16) {
               const bf16x8 bv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(ah) + 8 * k);
 #pragma unroll
               for (int e = 0; e < 8; ++e) xv[e] = (float)bv[e];
@@ -1318,6 +1436,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #ifdef TCN_ONE  // resource checks only (tools): the production kernels of both widths, nothing launchable
 template __global__ void k_tcn<LD_RECURSIVE, PREC_F16X3, false, 2, false, false, 2>(TcnArgs);
 template __global__ void k_tcn<LD_RECURSIVE, PREC_F16X3, false, 2, false, false, 1>(TcnArgs);
+template __global__ void k_tcn<LD_RECURSIVE, PREC_F32, false, 0, false, false, 1>(TcnArgs);
 #else
 template <int PRE, int LQ, bool LG>
 static hipError_t launch_tcn_pre(const TcnArgs& a, int grid, hipStream_t s) {
@@ -1364,7 +1483,9 @@ static hipError_t launch_tcn2_pre(const TcnArgs& a, int grid, hipStream_t s) {
 
 template <int PRE, int LQ>
 static hipError_t launch_tcn_lg(const TcnArgs& a, int grid, hipStream_t s) {
-  if (a.nsl == 2) return launch_tcn2_pre<PRE, LQ>(a, grid, s);
+  if constexpr (PRE != PREC_F32) {
+    if (a.nsl == 2) return launch_tcn2_pre<PRE, LQ>(a, grid, s);
+  }
   return a.G > FG_WAVE ? launch_tcn_pre<PRE, LQ, true>(a, grid, s) : launch_tcn_pre<PRE, LQ, false>(a, grid, s);
 }
 
@@ -1384,6 +1505,7 @@ hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
       return hipErrorInvalidValue;
     case PREC_F16: return launch_tcn_lg<PREC_F16, 0>(a, grid, s);
     case PREC_BF16: return launch_tcn_lg<PREC_BF16, 0>(a, grid, s);
+    case PREC_F32: return a.nsl == 1 ? launch_tcn_lg<PREC_F32, 0>(a, grid, s) : hipErrorInvalidValue;
   }
   return hipErrorInvalidValue;
 }
@@ -1416,6 +1538,7 @@ static int blocks_per_cu_nsl(int ln_mode, int prec, int lo) {
                      : (lo == 2 ? blocks_per_cu_pre<PREC_F16X3, 2, NSL>(ln_mode) : blocks_per_cu_pre<PREC_F16X3, 0, NSL>(ln_mode));
     case PREC_F16: return blocks_per_cu_pre<PREC_F16, 0, NSL>(ln_mode);
     case PREC_BF16: return blocks_per_cu_pre<PREC_BF16, 0, NSL>(ln_mode);
+    case PREC_F32: if constexpr (NSL == 1) return blocks_per_cu_pre<PREC_F32, 0, 1>(ln_mode); else return 0;
   }
   return 0;
 }

@@ -189,6 +189,37 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   }
   stamp(2);
 
+  // side outputs of the owned frames, bin-major [bs][k][f] (IP_OWN consecutive frames per bin): est from the
+  // rows, sigmoid(mask) recomputed from the masks (read again: side path only)
+  auto side_outputs = [&](bool unit_gain) {
+    constexpr int NI = (2 * NBIN * IP_OWN + 511) / 512;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = tid + j * 512;
+      const int sp = i / (NBIN * IP_OWN), rem = i - sp * (NBIN * IP_OWN);
+      const int k = rem / IP_OWN, fo = rem - k * IP_OWN;
+      const int f = f0 + fo;
+      if (i < 2 * NBIN * IP_OWN && f < T) {
+        const size_t o = (((size_t)b * 2 + sp) * NBIN + k) * T + f;
+        if (a.est_out) {
+          const float2 e = spec[sp][fo + 1][k];
+          const float gg = unit_gain ? 1.f : gain[sp][fo + 1];
+          st_out(a.est_out + o, poison ? make_float2(qnan, qnan) : make_float2(gg * e.x, gg * e.y));
+        }
+        if (a.mask_out)
+          st_out(a.mask_out + o, poison ? qnan : sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]));
+      }
+    }
+  };
+  // Without VAD filtering of the estimates the gain is 1 on every frame (est = X m): the side outputs go out now,
+  // so their stores drain under the VAD tail and the transforms (the same values as after the tail: gain * e with
+  // gain = 1 is e)
+  const bool early = (a.est_out || a.mask_out) && !(vad && a.kw_enabled && a.filt);
+  if (early) {
+    lds_sync();  // every row of spec written
+    side_outputs(true);
+  }
+
   // 0) VAD tail (model/model.py:160-179,444-457) for the frames of both speakers
   if (vad) {
     float g = 0.f, be = 0.f;
@@ -257,27 +288,8 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   lds_sync();
   stamp(3);
 
-  // side outputs of the owned frames, bin-major [bs][k][f] (IP_OWN consecutive frames per bin): est from the
-  // rows, sigmoid(mask) recomputed from the masks (read again: side path only)
-  if (a.est_out || a.mask_out) {
-    constexpr int NI = (2 * NBIN * IP_OWN + 511) / 512;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int i = tid + j * 512;
-      const int sp = i / (NBIN * IP_OWN), rem = i - sp * (NBIN * IP_OWN);
-      const int k = rem / IP_OWN, fo = rem - k * IP_OWN;
-      const int f = f0 + fo;
-      if (i < 2 * NBIN * IP_OWN && f < T) {
-        const size_t o = (((size_t)b * 2 + sp) * NBIN + k) * T + f;
-        if (a.est_out) {
-          const float2 e = spec[sp][fo + 1][k];
-          const float gg = gain[sp][fo + 1];
-          st_out(a.est_out + o, poison ? make_float2(qnan, qnan) : make_float2(gg * e.x, gg * e.y));
-        }
-        if (a.mask_out)
-          st_out(a.mask_out + o, poison ? qnan : sigmoid_f(a.masks[((size_t)b * a.Tp + f) * MOUT_PAD + sp * NBIN + k]));
-      }
-    }
+  if ((a.est_out || a.mask_out) && !early) {  // after the VAD gains (filtered estimates)
+    side_outputs(false);
     lds_sync();  // the transforms below overwrite the rows
   }
   // 2) inverse real FFT of every computed frame in its own row: 16 lanes per transform, transforms

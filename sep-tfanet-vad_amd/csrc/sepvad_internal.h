@@ -305,6 +305,9 @@ constexpr int PB_SIZE = 4904;                                      // multiple o
 constexpr size_t WF_W1L = 65536, WF_W2H = 131072, WF_W2L = 262144, WF_BLOCK = 393216;  // halves
 // single-plane (PREC_F16 / PREC_BF16) blobs: conv1d (256x256) | res_out (256x512)
 constexpr size_t WS_W2 = 65536, WS_BLOCK = 196608;  // halves
+// fused TCN, PREC_F32: conv1d (256x256) | res_out (256x512) as fp32 fragments (8 floats per lane per K step), in
+// __half units of the blob pointer
+constexpr size_t WS32_W2 = 2 * 65536, WS32_BLOCK = 2 * 196608;
 // F16X3 with an e4m3 lo plane (k_tcn default, SEPVAD_WLO_E4M3): conv1d hi (256x256 halves) | conv1d lo (256x256
 // bytes) | res_out hi (256x512 halves) | res_out lo (bytes). A lo byte is e4m3fn(lo * 2^WQ_LO_SHIFT): |lo| <= 2^-12 of
 // the row-scaled weight, so the stored value is <= 2^7 (e4m3 max 448) and keeps 4 significant bits down to 2^-25.
@@ -349,6 +352,7 @@ struct TcnArgs {
   // sum_c masks[t][s 257 + c] w1[o][c][k], zero for t >= T; B planes in fragment order, per-column scale; bin 256's
   // term w1[o][256][k] (hvny[4 k + o]) in fp32
   const __half* hvwh; const __half* hvwl; const float* hvwscale; const float* hvny;
+  const float* hvwf;     // PREC_F32: the VAD conv1_1 weights as fp32 fragments (the order of hvwh)
   float hvsx;            // range scale of the masks tile as the VAD GEMM's A operand (undone by hvwscale)
   float* hvP;            // nullable [B][2][Tp][HEAD_VAD_N]
   unsigned long long* hprobe;  // nullable diagnostics (SEPVAD_TAIL_PROBE): [grid][8] fused-head phase stamps

@@ -180,6 +180,8 @@ __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, int idx,
     lo[idx] = (_Float16)(v - (float)h);
   } else if constexpr (PRE == PREC_F16) {
     hi[idx] = (_Float16)v;
+  } else if constexpr (PRE == PREC_F32) {  // one fp32 plane (idx in floats)
+    reinterpret_cast<float*>(hi)[idx] = v;
   } else {
     reinterpret_cast<__bf16*>(hi)[idx] = (__bf16)v;
   }
@@ -250,6 +252,8 @@ __device__ __forceinline__ void split_store_rows(_Float16* hi, _Float16* lo, int
   } else if constexpr (PRE == PREC_F16) {
     const f16x2v h = __builtin_convertvector(v, f16x2v);
     hi[idx] = h.x; hi[idx + ld] = h.y;
+  } else if constexpr (PRE == PREC_F32) {  // (idx, ld in floats)
+    reinterpret_cast<float*>(hi)[idx] = v.x; reinterpret_cast<float*>(hi)[idx + ld] = v.y;
   } else {
     const bf16x2v h = __builtin_convertvector(v, bf16x2v);
     reinterpret_cast<__bf16*>(hi)[idx] = h.x; reinterpret_cast<__bf16*>(hi)[idx + ld] = h.y;
@@ -261,6 +265,10 @@ __device__ __forceinline__ void split_store_rows(_Float16* hi, _Float16* lo, int
 // idx = the lane's element for frame tl (as split_store_rows); every lane of the wave must take part (DPP).
 template <int PRE>
 __device__ __forceinline__ void split_store_rows_pk(_Float16* hi, _Float16* lo, int idx, int ld, f32x2 v, bool odd) {
+  if constexpr (PRE == PREC_F32) {  // 32-bit values already: plain stores (idx, ld in floats)
+    split_store_rows<PRE>(hi, lo, idx, ld, v);
+    return;
+  }
   const unsigned sel = odd ? 0x03020706u : 0x05040100u;  // odd: {partner.y, own.y}; even: {own.x, partner.x}
   const int at = odd ? idx + ld - 1 : idx;                // 4-byte aligned (m - 1 even / m even)
   auto put = [&](_Float16* plane, unsigned own) {

@@ -251,15 +251,29 @@ def test_whole_file_forwards_stay_fused(N, nets, state_dicts):
     check_vad_labels(vf[:1].cpu().numpy(), v_ref.numpy())
 
 
-def test_fp32_gemms_use_multikernel(nets):
-    net = nets["with_vad"]
+@pytest.mark.parametrize("cname", CONFIGS)
+def test_fp32_gemms_run_fused(cname, nets, state_dicts):
+    """The exact-fp32 arm on the fused schedule (k_tcn<PREC_F32>: v_mfma_f32_32x32x2_f32 on fp32 operands, the fp32
+    weights streamed, reference model/model.py:104,114,324): fused, within the fp32 gates of the oracle, and within
+    SCHED_TOL of the multi-kernel fp32 schedule (the same fp32 products, summed in a different order)."""
+    from oracle.torch_ref import OracleModel
+    from sep_tfanet_vad_amd import synth
+    net = nets[cname]
     net.native_precision = "fp32"
     try:
-        x = torch.rand(2, 8000, device=DEV) * 1.8 - 0.9
-        _, _, _, used = _run(net, x, True)
-        assert not used
+        x = torch.from_numpy(synth.make_batch(3, 32000, 515)[0])
+        sf, vf, _, used = _run(net, x.to(DEV), True)
+        assert used
+        sm, vm, _, used_m = _run(net, x.to(DEV), False)
+        assert not used_m
     finally:
         net.native_precision = "f16x3"
+    assert (sf - sm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    om = OracleModel(config_of(cname), state_dicts[cname], torch.float32)
+    s_ref, v_ref, _ = om(x[:2])
+    assert np.abs(sf[:2].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    check_vad_labels(vf[:2].cpu().numpy(), v_ref.numpy())
 
 
 def test_handoff_protocols_bitwise_identical(nets):
