@@ -152,7 +152,7 @@ struct sepvad_model {
   int split = 1;
   hipStream_t sub[MAX_SPLIT] = {};
   hipEvent_t fork = nullptr, join[MAX_SPLIT] = {};
-  // fused persistent TCN (fused.hip): one launch for all blocks when the GEMMs are not fp32 and T <= 8192
+  // fused persistent TCN (tcn_kernel.h): one launch for all blocks when the GEMMs are not fp32 and T <= 8192
   bool fused = true;
   int tcn_cap = 0;              // co-resident k_tcn workgroups (CUs x workgroups per CU), max over precisions
   int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
@@ -326,7 +326,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
             fh[q] = hi[src];
             fl[q] = lo[src];
             fb[q] = bf[src];
-            // exact: a power-of-two row scale (PREC_F32: v_mfma_f32_32x32x2_f32 pairs k = 8 h + j, fused.hip)
+            // exact: a power-of-two row scale (PREC_F32: v_mfma_f32_32x32x2_f32 pairs k = 8 h + j, tcn_kernel.h)
             ff[q] = w32[src] * srow[src / cin];
           }
     p.ff32 = pk.add(ff);
@@ -478,7 +478,7 @@ LoadSpec residual_spec(const sepvad_model* h, const Workspace& w, int i, const f
   return ld;
 }
 
-// Weight/parameter blobs, hand-off buffers and residency capacity of the fused TCN (fused.hip):
+// Weight/parameter blobs, hand-off buffers and residency capacity of the fused TCN (tcn_kernel.h):
 // per block the fragment-ordered fp16 hi/lo weights (WF_*) and one float parameter blob (PB_*), both
 // contiguous over blocks so the kernel addresses block i with uniform arithmetic (no pointer loads).
 int init_fused(sepvad_model* h, const Packer& pk) {
@@ -1047,7 +1047,7 @@ int env_int(const char* name, int dflt) {
 
 // Progress of concurrent fused launches (include/sepvad.h: concurrent forwards on different streams are allowed).
 // A k_tcn group waits for all of its G members, and the grid is dealt in order, so a launch progresses as long as
-// 8 G of its workgroups are resident (fused.hip header). Two launches that each need more than half the chip for
+// 8 G of its workgroups are resident (tcn_kernel.h header). Two launches that each need more than half the chip for
 // that can each hold part of the CUs and wait on each other until the give-up bound. Such "big" launches (long
 // utterances) are therefore ordered across streams, process-wide per device: each waits on the previous one's
 // completion event (stream-ordered, no host sync). Launches of small groups need no ordering: any resident prefix
@@ -1055,7 +1055,7 @@ int env_int(const char* name, int dflt) {
 int tcn2_cap_of(const sepvad_model* h) {
   return h->prec == PREC_F16X3 && h->lo8 ? h->tcn2_cap_q[h->lo8] : h->tcn2_cap_p[h->prec];
 }
-// Slices (32-frame members) per k_tcn workgroup for a batch of B utterances of G members: two (64 frames, fused.hip
+// Slices (32-frame members) per k_tcn workgroup for a batch of B utterances of G members: two (64 frames, tcn_kernel.h
 // TcnSmem2) once one-slice workgroups would need more than one round of the chip (B * G > capacity), so every weight
 // fragment a CU streams feeds 64 frames instead of 32; the two give the same bits, so the choice never changes a
 // result. SEPVAD_TCN_SLICES = 1 | 2 forces one (2 where the two-slice kernel applies: G even, G <= FG_WAVE).
@@ -1195,7 +1195,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   // the VAD conv1_1 as the output head's second GEMM (raw masks in; the masked-speakers variant reads |X| too)
   const bool vad_in_head = use_fused && has_vad && !c.final_vad_masked_speakers;
   if (use_fused) {
-    // persistent launches of the whole TCN (fused.hip), the output head inside them
+    // persistent launches of the whole TCN (tcn_kernel.h), the output head inside them
     const int nsl = h->tdump ? 1 : tcn_slices(h, B, G);  // (the parity-dump instantiation is one-slice only)
     const int cap = nsl == 2 ? tcn2_cap_of(h) : tcn_cap_of(h);
     h->last_nsl = nsl;
@@ -1239,7 +1239,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     // diagnostics (SEPVAD_TCN_MAX_GROUPS): fewer groups per launch, so each loops over more utterances (tests reach
     // the epoch budget below with small batches)
     if (const int mg = env_int("SEPVAD_TCN_MAX_GROUPS", 0); mg > 0 && mg < ngroups) ngroups = mg;
-    // epochs per launch and group (fused.hip): 1 (XCD ids) + per utterance 4 per block with TF-attention (P1..P4;
+    // epochs per launch and group (tcn_kernel.h): 1 (XCD ids) + per utterance 4 per block with TF-attention (P1..P4;
     // 3 without) + 1 for the output head (P5). The tag is salt << TCN_EPOCH_BITS | epoch, so the last epoch of a
     // launch must stay below 2^TCN_EPOCH_BITS: an epoch carried into the salt bits would repeat the next launch's tags
     // (SEPVAD_TCN_MAX_ITER lowers it: tests force several launches per forward)

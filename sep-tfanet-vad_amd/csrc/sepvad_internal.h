@@ -274,7 +274,7 @@ struct VadAccArgs {
 hipError_t launch_vad_acc(const VadAccArgs& a, hipStream_t s);
 hipError_t launch_normalize(const NormArgs& a, hipStream_t s);
 
-// ---- fused persistent TCN (fused.hip) ----
+// ---- fused persistent TCN (tcn_kernel.h; dispatch fused.hip, instantiations fused_inst.hip) ----
 constexpr int FR = 32;          // frames per workgroup
 #ifndef SEPVAD_FG_MAX
 #define SEPVAD_FG_MAX 256

@@ -1,4 +1,4 @@
-// Device helpers of the persistent TCN kernel (fused.hip k_tcn):
+// Device helpers of the persistent TCN kernel (tcn_kernel.h k_tcn):
 // MFMA operand types, wave-uniform buffer descriptors, the tagged 8-byte hand-off words ("data is its own
 // flag", cdna_hip_programming.md Guideline 16 R2) with bounded polls, DPP lane reductions and the fp16 hi/lo
 // operand split.
@@ -397,7 +397,7 @@ __device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, do
 
 // Diagnostics (SEPVAD_TCN_DELAY = n): member 0 of every group sleeps n x ~8k cycles at the call sites (after a
 // publish, before the matching polls), so the other members run ahead into the next epochs: the hand-off words of
-// different epochs must not alias while a late member still polls them (fused.hip GW_*). 0 in production.
+// different epochs must not alias while a late member still polls them (tcn_kernel.h GW_*). 0 in production.
 __device__ __forceinline__ void tcn_delay(int g) {
   const unsigned n = kargs()->dbg_delay;
   if (n != 0 && g == 0)

@@ -281,7 +281,7 @@ def test_shortest_input_and_too_short_input(net, state_dicts):
 def test_late_member_never_gives_up(net, B, N):
     """Member 0 of every group sleeps after its P1 and P3 publishes (SEPVAD_TCN_DELAY), so the other members run ahead
     into the next epochs while it has not yet polled the earlier ones: no hand-off word a late member still polls may
-    be overwritten (fused.hip GW_* layout). No give-up, bitwise the undelayed outputs; G = 4 and G = 33 (cross-XCD)."""
+    be overwritten (tcn_kernel.h GW_* layout). No give-up, bitwise the undelayed outputs; G = 4 and G = 33 (cross-XCD)."""
     from sep_tfanet_vad_amd import synth
     h = net.native_handle(DEV)
     x = torch.from_numpy(synth.make_batch(B, N, 515)[0]).to(DEV)

@@ -1,4 +1,4 @@
-"""The fused persistent TCN (csrc/fused.hip, one launch for all 24 blocks) against the oracle, the
+"""The fused persistent TCN (csrc/tcn_kernel.h, one launch for all 24 blocks) against the oracle, the
 reference goldens and the multi-kernel schedule, over the group sizes it supports (G = ceil(T/32) =
 1..32 workgroups per utterance: one-wave and LDS statistic finishes, one- and two-pass moment polls), batches larger than one resident wave of groups, and the fallback.
 
@@ -165,7 +165,7 @@ def _run_slices(net, x, slices, monkeypatch, prec="f16x3"):
 @pytest.mark.parametrize("cname", CONFIGS)
 @pytest.mark.parametrize("N", [12345, 32000, 48000, 64000, 96000, 130816])
 def test_two_slices_bitwise_equal_one_slice(cname, N, nets, monkeypatch):
-    """Two-slice workgroups (fused.hip NSL = 2: 64 frames, one weight stream for both 32-frame tiles, the depthwise conv
+    """Two-slice workgroups (tcn_kernel.h NSL = 2: 64 frames, one weight stream for both 32-frame tiles, the depthwise conv
     and res_out GEMM in two K halves) against one-slice workgroups: every member statistic is reduced in the one-slice
     order, so sep, vad and est are bitwise equal. G = 2, 4, 6, 8, 12, 16 members (T = 49 .. 512), both LN modes
     (recursive: config_with_vad, residual: config_without_vad)."""

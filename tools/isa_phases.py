@@ -1,4 +1,4 @@
-"""Static instruction census per k_tcn phase from a -DTCN_MARK -DTCN_ONE build (fused.hip TMARK comments at the phase
+"""Static instruction census per k_tcn phase from a -DTCN_MARK -DTCN_ONE build (tcn_kernel.h TMARK comments at the phase
 points of TPROBE). usage: python tools/isa_phases.py <file.s> <mangled-kernel-substring>
 Prints, per phase interval [marker a -> next marker], the count of VALU (incl. packed and lane ops), MFMA, LDS, VMEM,
 SALU and waitcnt instructions. Static counts: inner loops (polls, member sums) count once."""

@@ -10,7 +10,7 @@ import numpy as np
 
 NAMES = ["conv1d GEMM", "epilogue+GN1 stats", "P1 publish+wait+halo", "dwconv+GN2 stats", "res_out GEMM",
          "P2 wait", "rowsum/colsum", "P3 publish+wait", "gates", "moments", "P4 publish+wait", "x' update"]
-# sub-phase stamps currently placed in fused.hip: slot 13 after the residual-LN affines (x' update
+# sub-phase stamps currently placed in tcn_kernel.h: slot 13 after the residual-LN affines (x' update
 # phase start), slot 14 after the next block's weight prefetch is issued
 SUB = [(13, 11, "x': moments->affines"), (14, 13, "x': prefetch issue"), (12, 14, "x': update+barrier")]
 if os.environ.get("TCN_SUB") == "1":  # library built with -DTCN_SUB=1: the stamps sit in the depthwise conv
