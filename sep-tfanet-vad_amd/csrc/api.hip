@@ -1429,6 +1429,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     vf.b1 = h->P(h->v_b1); vf.alpha = h->v_a;
     vf.g = h->P(h->v_g); vf.be = h->P(h->v_b); vf.eps = 1e-8f;
     vf.feat = w.vy;
+    vf.out_rec = T > VF_ONE_T ? w.rec_vad : nullptr;  // long utterances: partial records, BN_1 in k_istft_pair
     HIPCHK(launch_vad_feat(vf, s));
   }
   if (has_vad && !vad_in_head) {
@@ -1456,11 +1457,11 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
       is.ret_smooth = kw_on && kw->return_smoothed_vad;
       is.thr = kw_on ? kw->threshold_activated_vad : 0.5f;
       is.vy = w.vy; is.w2 = h->P(h->v_w2); is.b2 = h->v_b2;
-      is.vy_norm = vad_in_head && !vad_taps_in_istft;
+      is.vy_norm = vad_in_head && !vad_taps_in_istft && T <= VF_ONE_T;
       if (vad_taps_in_istft) {
         is.vP = w.vP; is.vb1 = h->P(h->v_b1); is.valpha = h->v_a; is.vy = nullptr;
       }
-      is.vgn = gn_src(w.rec_vad, Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
+      is.vgn = gn_src(w.rec_vad, vad_in_head ? vf_nrec(Tp) : Tp / VAD_ROWS, 2, 0, h->P(h->v_g), h->P(h->v_b), 1e-8f);
       is.vad_out = out->vad ? out->vad + u2 * T : w.vad;
     }
     is.est_out = out->est ? (float2*)out->est + u2 * NBIN * T : nullptr;

@@ -183,7 +183,12 @@ struct VadFeatArgs {     // k_vad_feat: conv1_1 finish + BN_1 from the output he
   const float* b1; float alpha;       // conv1_1 bias [4], relu_1 PReLU
   const float* g; const float* be; float eps;  // BN_1 affine, eps
   float* feat;           // [B][2][4][Tp] normalised features (the k_istft VAD tail's input)
+  double* out_rec;       // T > VF_ONE_T: [B*2][vf_nrec(Tp)][2] BN_1 partial records; feat is then un-normalised
 };
+// k_vad_feat finishes BN_1 itself up to VF_ONE_T frames (one workgroup per utterance and speaker); longer utterances run
+// k_vad_feat_rec (one workgroup per VF_ROWS frames, partial records, BN_1 applied by k_istft_pair)
+constexpr int VF_ONE_T = 1024, VF_ROWS = 128;
+__host__ __device__ inline int vf_nrec(int Tp) { return (Tp + VF_ROWS - 1) / VF_ROWS; }
 hipError_t launch_vad_feat(const VadFeatArgs& a, hipStream_t s);
 
 struct IstftArgs {

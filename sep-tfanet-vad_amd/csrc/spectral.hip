@@ -230,8 +230,7 @@ __global__ __launch_bounds__(256) void k_vad1(Vad1Args a) {
 // (utterance, speaker): y[t][o] = sum_k P[t - 2 + k][4 k + o] (zero outside [0, T)), v = PReLU(y + b1),
 // BN_1 = GroupNorm(1, 4) over [4, T] (block sums in double, wave order), feat = v * s[o] + h[o] for
 // k_istft_pair's VAD tail (model/model.py:158-176).
-// NI items (t, o) per thread: 4 for T <= 256, 16 for T <= 1024, 64 for T <= 4096, 128 for T <= 8192 (long utterances on
-// the fused schedule).
+// NI items (t, o) per thread: 4 for T <= 256, 16 for T <= VF_ONE_T (longer utterances: k_vad_feat_rec).
 template <int NI>
 __global__ __launch_bounds__(256) void k_vad_feat(VadFeatArgs a) {
   __shared__ float red[2 * 16];
@@ -268,12 +267,42 @@ __global__ __launch_bounds__(256) void k_vad_feat(VadFeatArgs a) {
   }
 }
 
+// k_vad_feat_rec: long utterances (T > VF_ONE_T). One workgroup per (utterance, speaker, VF_ROWS frames): the same
+// conv1_1 + PReLU items as k_vad_feat, written un-normalised, and the chunk's BN_1 partial record {sum, sumsq} (wave
+// sums, then the 4 wave totals in double in wave order); k_istft_pair sums the records in record order and applies BN_1
+// (its vy_norm = 0 path). One workgroup per utterance and speaker took 35 us for two 60 s files (4 workgroups).
+__global__ __launch_bounds__(256) void k_vad_feat_rec(VadFeatArgs a) {
+  __shared__ float red[2 * 16];
+  constexpr int NI = 4 * VF_ROWS / 256;
+  const int tid = threadIdx.x, bs = blockIdx.x, T = a.T, t0 = blockIdx.y * VF_ROWS;
+  const float* P = a.vP + (size_t)bs * a.Tp * HEAD_VAD_N;
+  float st[2] = {0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NI; ++it) {
+    const int i = tid + 256 * it, t = t0 + (i >> 2), o = i & 3;
+    float y = 0.f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int tt = t - 2 + k;
+      y += (t < T && tt >= 0 && tt < T) ? P[(size_t)tt * HEAD_VAD_N + 4 * k + o] : 0.f;
+    }
+    const float v = prelu_f(y + a.b1[o], a.alpha);
+    if (t < a.Tp) a.feat[((size_t)bs * 4 + o) * a.Tp + t] = t < T ? v : 0.f;
+    if (t < T) { st[0] += v; st[1] += v * v; }
+  }
+  block_reduce_store<2>(st, red, a.out_rec + ((size_t)bs * vf_nrec(a.Tp) + blockIdx.y) * 2);
+}
+
 hipError_t launch_vad_feat(const VadFeatArgs& a, hipStream_t s) {
   if (a.T < 1 || a.T > 8192) return hipErrorInvalidValue;
-  if (a.T <= 256) hipLaunchKernelGGL(k_vad_feat<4>, dim3(a.B * 2), dim3(256), 0, s, a);
-  else if (a.T <= 1024) hipLaunchKernelGGL(k_vad_feat<16>, dim3(a.B * 2), dim3(256), 0, s, a);
-  else if (a.T <= 4096) hipLaunchKernelGGL(k_vad_feat<64>, dim3(a.B * 2), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_vad_feat<128>, dim3(a.B * 2), dim3(256), 0, s, a);
+  if (a.T > VF_ONE_T) {
+    if (a.out_rec == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_vad_feat_rec, dim3(a.B * 2, vf_nrec(a.Tp)), dim3(256), 0, s, a);
+  } else if (a.T <= 256) {
+    hipLaunchKernelGGL(k_vad_feat<4>, dim3(a.B * 2), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_vad_feat<16>, dim3(a.B * 2), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 
