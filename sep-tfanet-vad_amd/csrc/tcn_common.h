@@ -395,6 +395,23 @@ __device__ __forceinline__ void member_moments_w(unsigned w, int base, int G, do
   gn_moments_f(s, ss, inv, eps, mu, rs);
 }
 
+// p[0] + p[s] + ... + p[(n - 1) s] summed in index order (the order of the plain loop, so the same bits), the LDS
+// loads issued 8 at a time: a runtime-count loop otherwise waits for each load before its add (a group of 118
+// members' records took ~100 cycles per member).
+__device__ __forceinline__ double seq_sum_lds(const double* p, int s, int n) {
+  double acc = 0.0;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(k + u) * s];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < n; ++k) acc += p[k * s];
+  return acc;
+}
+
 // Diagnostics (SEPVAD_TCN_DELAY = n): member 0 of every group sleeps n x ~8k cycles at the call sites (after a
 // publish, before the matching polls), so the other members run ahead into the next epochs: the hand-off words of
 // different epochs must not alias while a late member still polls them (tcn_kernel.h GW_*). 0 in production.

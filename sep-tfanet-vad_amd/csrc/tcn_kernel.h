@@ -544,11 +544,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       gpoll<1>(p, a.tag0 + 1, v, a);
       if (tid < G) sm.gw[tid] = v[0];
       __syncthreads();
-      bool same = a.xmode == 0, sub = a.xmode == 0;
-      for (int mm = 0; mm < G; ++mm) {
-        same = same && sm.gw[mm] == sm.gw[0];
-        if (LG) sub = sub && (mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8]);
+      // every member's id against member 0's (and, long groups, against its leader's) by the threads in parallel, then a
+      // workgroup AND (a serial loop over the members in every thread took ~5 us at G = 118)
+      int same_t = 1, sub_t = 1;
+      for (int mm = tid; mm < G; mm += NTHR) {
+        same_t &= sm.gw[mm] == sm.gw[0];
+        if (LG) sub_t &= mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8];
       }
+      const bool same = a.xmode == 0 && __syncthreads_and(same_t) != 0;
+      const bool sub = a.xmode == 0 && (!LG || __syncthreads_and(sub_t) != 0);
       // wave-uniform (the words in LDS are the same for every lane): a per-lane flag in a VGPR made every hand-off
       // store a divergent branch, and at two slices hipcc spilled it and reloaded it behind vmcnt(0)
       l2 = __builtin_amdgcn_readfirstlane((int)same) != 0;
@@ -1113,9 +1117,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             __syncthreads();
             if (wave_s == 0) {
               const double* gd = reinterpret_cast<const double*>(sm.gw);
-              double sj = 0.0;
               const int j = lane < NMOM ? lane : 0;
-              for (int k = 0; k < nsub; ++k) sj += gd[NMOM * k + j];
+              const double sj = seq_sum_lds(gd + j, NMOM, nsub);
               if (lane < NMOM) gputd(slot(g, e4) + GW_SUB4 + 2 * lane, tag4, sj, l2);
             }
             __syncthreads();  // the leader's words read before the leaders' partials land in sm.gw
@@ -1158,11 +1161,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // lane j < NMOM of every wave sums moment j over the members (one LDS load per member per wave),
         // then the 11 sums become wave-uniform by readlane
         const double* gd = reinterpret_cast<const double*>(sm.gw);
-        double sj = 0.0;
-        {
-          const int j = lane < NMOM ? lane : 0;
-          for (int mm = 0; mm < (tree ? 8 : G); ++mm) sj += gd[NMOM * mm + j];  // members, or the 8 leaders' partials
-        }
+        const double sj = seq_sum_lds(gd + (lane < NMOM ? lane : 0), NMOM, tree ? 8 : G);  // members, or the 8
+                                                                                              // leaders' partials
         double ms[NMOM];
 #pragma unroll
         for (int j = 0; j < NMOM; ++j) ms[j] = readlane_d(sj, j);
@@ -1265,9 +1265,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       __syncthreads();
       if (tidh < 2) {  // GroupNorm statistics of PReLU(x') over the utterance: the members' records in member order
         const double* gd = reinterpret_cast<const double*>(sm.gw);
-        double sd = 0.0;
-        for (int mm = 0; mm < G; ++mm) sd += gd[2 * mm + tidh];
-        sm.dred[8 + tidh] = sd;
+        sm.dred[8 + tidh] = seq_sum_lds(gd + tidh, 2, G);
       }
       __syncthreads();
       // A = GN_out(PReLU(x')) into LDS (scaled by hsx, undone by the weights' row scale)
