@@ -1221,8 +1221,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.force_err = env_int("SEPVAD_TCN_FORCE_GIVEUP", 0);
     ta.dbg_delay = (unsigned)std::max(0, env_int("SEPVAD_TCN_DELAY", 0));
     ta.dump_blk = std::max(0, std::min(h->nblk - 1, env_int("SEPVAD_TCN_DUMP_BLOCK", 0)));
+    // every group the chip holds (the kernel puts the groups of 8 * Gt * floor(groups / 8) blocks on one XCD each and the
+    // rest, fewer than 8, on consecutive blocks; SEPVAD_TCN_ALIGN8=1: whole multiples of 8 groups only, as in round 4)
     int ngroups = std::min(B, cap / Gt);
-    if (ngroups >= 8) ngroups -= ngroups % 8;
+    if (ngroups >= 8 && env_int("SEPVAD_TCN_ALIGN8", 0)) ngroups -= ngroups % 8;
     // the output head, inside k_tcn after each utterance's last block (its lo plane in the blocks' format)
     ta.hg = h->P(h->out_g); ta.hbe = h->P(h->out_b); ta.hsx = h->out_sx;
     ta.hwh = h->prec == PREC_F32 ? reinterpret_cast<const __half*>(h->P(h->wout_spk.ff32))
@@ -1261,7 +1263,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     for (int u0 = 0; u0 < B; u0 += per_launch) {
       const int Bl = std::min(per_launch, B - u0);
       const int ng = std::min(ngroups, Bl);
-      const int ngl = ng >= 8 ? ng - ng % 8 : ng;
+      const int ngl = ng;
       ta.tag0 = (gsalt_lo + gsalt_n++) << TCN_EPOCH_BITS;
       ta.B = Bl;
       ta.S0 = w.S0 + (size_t)u0 * Tp * CH;

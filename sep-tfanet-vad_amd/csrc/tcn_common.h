@@ -70,7 +70,10 @@ __device__ __forceinline__ void giveup(const TcnArgs& a) {
 template <int N>
 __device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned (&tag)[N], unsigned (&v)[N],
                                        const TcnArgs& a) {
-  const u64* const dummy = a.gran;  // any readable 8-byte word
+  // the word a null entry reads instead: an unused word past GW_SUB4 in slot pair blockIdx.x (gran holds a slot pair per
+  // member, >= the grid), a line of this workgroup's own -- not one word for the whole launch, which every wave of
+  // every CU read on every poll pass (a single hot L2 line)
+  const u64* const dummy = a.gran + (size_t)blockIdx.x * 2 * NGR + 2 * NGR - 4;
   unsigned spins = 0;
   for (;;) {
     u64 x[N];
@@ -167,7 +170,8 @@ constexpr int GW_P4 = 4;                 // P4: the moment record, 11 doubles as
 // every P1 word (without TF-attention a block has three epochs, so P1 and P4 share a slot parity every other block)
 constexpr int GW_SUB3 = GW_COL + FR;     // [256] a leader's partial row sums
 constexpr int GW_SUB4 = GW_SUB3 + CH;    // [22] a leader's partial moment record
-static_assert(GW_SUB4 + 2 * NMOM <= NGR && GW_P4 >= GW_STAT + 4, "granule slot size / P2-P4 separation");
+static_assert(GW_SUB4 + 2 * NMOM <= NGR - 4 && GW_P4 >= GW_STAT + 4,
+              "granule slot size (the last 4 words unused: gpollt's dummy word) / P2-P4 separation");
 
 
 // One GEMM operand value into LDS in the format PRE multiplies: fp16 hi/lo split (F16X3), fp16 (F16) or

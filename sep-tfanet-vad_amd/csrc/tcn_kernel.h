@@ -439,15 +439,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   const int G = a.G;        // members (32-frame slices) per utterance
   const int GW = G / NSL;   // workgroups per group
   if (TCN_PRIO && wave_s >= 4) __builtin_amdgcn_s_setprio(1);
-  // block -> (group, workgroup g of the group): a group's workgroups on one XCD when the grid is a multiple of 8*GW
+  // block -> (group, workgroup g of the group): the groups of the first 8 * GW * floor(groups / 8) blocks each on one
+  // XCD (blocks b, b + 8, ...: round-robin dispatch), the remaining groups (fewer than 8) on consecutive blocks, which
+  // span XCDs (their hand-offs write through; speed only). Those take the highest group ids: with u = grp, grp +
+  // groups, ... they never take an extra utterance.
   int grp, g;
-  if (gridDim.x % (8 * GW) == 0) {
-    const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
-    grp = (idx / GW) * 8 + x;
-    g = idx % GW;
-  } else {
-    grp = blockIdx.x / GW;
-    g = blockIdx.x % GW;
+  {
+    const int na = (int)(gridDim.x / (8 * GW)) * 8 * GW;  // blocks of the XCD-aligned groups
+    if ((int)blockIdx.x < na) {
+      const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
+      grp = (idx / GW) * 8 + x;
+      g = idx % GW;
+    } else {
+      grp = (int)blockIdx.x / GW;  // (na is a multiple of GW: group ids na / GW, ...)
+      g = (int)blockIdx.x % GW;
+    }
   }
   const int ngroups = gridDim.x / GW;
   const int m0 = NSL * g;  // this workgroup's first member: slice s is member m0 + s
