@@ -539,7 +539,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
     if (TP_ON && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 6) * 16 + 15] = wall_clock64();
-    reduce_records(rec_src(a.ln, u, 2), rec_none(), sm.dred);
+    // TCN.LN records of utterance u (k_stft_gate: one per 16 frames): every value staged in LDS by one thread each (all
+    // loads in flight at once), summed below in record order by threads j < 2 -- reduce_records' order, the same bits
+    // (its batches of 16 dependent loads took ~6 us for the 236 records of a 60 s file). H is free until the blocks.
+    double* const lnst = reinterpret_cast<double*>(sm.H);
+    const RecSrc lnr = rec_src(a.ln, u, 2);
+    static_assert(2 * (FG_MAX * FR / GATE_ROWS) * sizeof(double) <= sizeof(sm.H), "staged LN records in H");
+    for (int i = tid; i < 2 * lnr.n; i += NTHR) lnst[i] = lnr.p[(size_t)(i >> 1) * lnr.rs + (i & 1)];
     if (TP_ON && tid == 0 && u == grp && a.nblk > 7) a.probe[((size_t)blockIdx.x * a.nblk + 7) * 16 + 15] = wall_clock64();
     if (u == grp) {
       // the members' XCD ids (write-through, epoch 1); if the whole group shares one XCD, every later
@@ -565,7 +571,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       sl2 = __builtin_amdgcn_readfirstlane((int)sub) != 0;
       if (TP_ON && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
     }
-    __syncthreads();  // LN record sums (sm.dred) complete
+    __syncthreads();  // staged LN records complete
+    if (tid < 2) sm.dred[tid] = seq_sum_lds(lnst + tid, 2, lnr.n);
+    __syncthreads();  // LN record sums (sm.dred) complete (the LN affine below may overwrite H: two-slice sm.c)
     if (TP_ON && tid == 0 && u == grp && a.nblk > 2) a.probe[((size_t)blockIdx.x * a.nblk + 2) * 16 + 15] = wall_clock64();
     {  // gn_affine with this iteration's thread id (channel tid < CH)
       float mu, rs;
