@@ -214,6 +214,31 @@ def test_two_slices_chosen_past_one_round_and_repeatable(nets):
         assert torch.equal(a_[sub], b_)
 
 
+def test_remainder_groups_span_xcds_bitwise(nets, monkeypatch):
+    """All groups the chip holds: at T = 188 (G = 6, two-slice workgroups, 3 per group) the chip holds 85 groups; the
+    kernel puts 80 of them on one XCD each and the remaining 5 on consecutive blocks (their hand-offs write through).
+    Bitwise the outputs of the round-4 launch shape (SEPVAD_TCN_ALIGN8=1: 80 groups) and of a small batch of the same
+    utterances (one-slice groups)."""
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(100, 48000, 5757)[0]).to(DEV)
+    outs = {}
+    for a8 in ("0", "1"):
+        monkeypatch.setenv("SEPVAD_TCN_ALIGN8", a8)
+        with torch.no_grad():
+            outs[a8] = net(x)
+        assert h.fused_slices() == 2
+    monkeypatch.delenv("SEPVAD_TCN_ALIGN8")
+    for a_, b_ in zip(outs["0"], outs["1"]):
+        assert torch.equal(a_, b_)
+    sub = [0, 84, 85, 99]  # group 0, the last remainder group, and the second round
+    with torch.no_grad():
+        small = net(x[sub])
+    for a_, b_ in zip(outs["0"], small):
+        assert torch.equal(a_[sub], b_)
+
+
 def test_inference_kw_on_fused(nets):
     g = load_golden("with_vad", "small")
     ikw = dict(filter_signals_by_smo_vad=True, filter_signals_by_unsmo_vad=False, length_smoothing_filter=3,
