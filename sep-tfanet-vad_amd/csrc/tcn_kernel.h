@@ -51,7 +51,10 @@ namespace sepvad {
 // scalar elementwise phases, separate P2 round, thread-finished GN moments, double GN finish, 11-term moments, burst
 // ring prefetch, LDS epilogue parameters -- live in the git history)
 #ifndef TCN_PRIO
-#define TCN_PRIO 0   // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md "Static priority for the younger half")
+// 1 (round 5): waves 4-7 at s_setprio 1 for the whole kernel (MI355X_MICROARCH.md "Static priority for the younger
+// half"): they share each SIMD's MFMA pipe with waves 0-3 and, without it, finish every GEMM last (the barrier after
+// the GEMM waits for them): k_tcn -2.4 % shader cycles at cfg 2, bitwise equal (profiles/r05_prio/). 0 = round 4.
+#define TCN_PRIO 1
 #endif
 #ifndef TCN_SUB
 #define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)

@@ -13,10 +13,13 @@ for r in 1 2; do
     python3 -c "import json; d=json.loads(open('$out/s.json').read().strip().splitlines()[-1]); print('$(basename $lib) $r', d['value'], d['ms_per_step'])"
   done
 done | tee $out/ab.txt
-rm -f $out/dump_*.npy.tmp; python3 -c "
-import numpy as np, glob
-a = np.load(glob.glob('$out/dump_$(basename $prev .so)*.npy')[0]); b = np.load(glob.glob('$out/dump_libsepvad*.npy')[0])
-print("stitched streams bitwise equal:", np.array_equal(a.view(np.uint32), b.view(np.uint32))) | tee -a $out/ab.txt
+python3 - $out $(basename $prev .so) <<'PY' | tee -a $out/ab.txt
+import glob, sys
+import numpy as np
+out, prev = sys.argv[1], sys.argv[2]
+a = np.load(glob.glob(f"{out}/dump_{prev}*.npy")[0]); b = np.load(glob.glob(f"{out}/dump_libsepvad*.npy")[0])
+print("stitched streams bitwise equal:", np.array_equal(a.view(np.uint32), b.view(np.uint32)))
+PY
 step stats && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --no-cpu-baseline --workload stream --steps 3 --warmup 1 > $out/prof.log 2>&1 \
 && python3 tools/kstats.py $(find $out/prof -name "*kernel_stats.csv" | head -1) | grep -v copyBuffer
 step done
