@@ -25,9 +25,12 @@ __global__ __launch_bounds__(PIT_THREADS) void k_pit_l1_partial(PitArgs a) {
   const long long beg = per * blockIdx.x;
   const long long end = min(total, beg + per);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  // fp32 per thread over a short strided range, then double across the block
-  for (long long i = beg + threadIdx.x; i < end; i += PIT_THREADS) {
-    const long long b = i / a.L, n = i % a.L;
+  // fp32 per thread over a short strided range, then double across the block. (b, n) of element i advance by
+  // PIT_THREADS per step with a carry into b (one 64-bit division per thread, not one per element: the per-element
+  // i / L, i % L made the kernel VALU-bound)
+  long long i = beg + threadIdx.x;
+  long long b = i / a.L, n = i - b * a.L;
+  for (; i < end; i += PIT_THREADS) {
     const float* e = a.est + (size_t)b * 2 * a.est_ld + n;
     const float* r = a.ref + (size_t)b * 2 * a.ref_ld + n;
     const float e0 = e[0], e1 = e[a.est_ld], r0 = r[0], r1 = r[a.ref_ld];
@@ -35,6 +38,8 @@ __global__ __launch_bounds__(PIT_THREADS) void k_pit_l1_partial(PitArgs a) {
     acc[1] += fabsf(e0 - r1);
     acc[2] += fabsf(e1 - r0);
     acc[3] += fabsf(e1 - r1);
+    n += PIT_THREADS;
+    while (n >= a.L) { n -= a.L; ++b; }
   }
   block_reduce_store<4>(acc, red, a.partial + (size_t)blockIdx.x * 4);
 }
