@@ -27,6 +27,15 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
   }
 }
 
+__device__ __forceinline__ void st_out(float4* p, float4 v) {
+  if constexpr (SEPVAD_NT) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 __device__ __forceinline__ float prelu_f(float x, float w) { return x > 0.f ? x : w * x; }
 
 #ifndef SEPVAD_DB_FAST

@@ -192,6 +192,39 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   // side outputs of the owned frames, bin-major [bs][k][f] (IP_OWN consecutive frames per bin): est from the
   // rows, sigmoid(mask) recomputed from the masks (read again: side path only)
   auto side_outputs = [&](bool unit_gain) {
+    if (a.est_out && !a.mask_out && T % 2 == 0) {
+      // the forward's est alone (T even: a row starts 16-B aligned): two frames per 16-B store where the pair is aligned
+      // (frames f0 + fo, f0 + fo + 1 with f0 + fo even), the odd one out alone -- half the store instructions of one
+      // frame per lane (the store phase is issue-bound: every workgroup of the round stores at once)
+      constexpr int NSL6 = (IP_OWN + 2) / 2;  // slots per (speaker, bin) row: 5 pairs and one single frame
+      constexpr int NI6 = (2 * NBIN * NSL6 + 511) / 512;
+      const int par = f0 & 1;
+#pragma unroll
+      for (int jj = 0; jj < NI6; ++jj) {
+        const int i = tid + jj * 512;
+        const int sp = i / (NBIN * NSL6), rem = i - sp * (NBIN * NSL6);
+        const int k = rem / NSL6, sl = rem - k * NSL6;
+        const int fo = par == 0 ? 2 * sl : (sl == 0 ? 0 : 2 * sl - 1);
+        int n = par == 0 ? (fo + 1 < IP_OWN ? 2 : 1) : (sl == 0 ? 1 : 2);
+        const int f = f0 + fo;
+        if (i < 2 * NBIN * NSL6 && f < T) {
+          if (f + 1 >= T) n = 1;
+          const size_t o = (((size_t)b * 2 + sp) * NBIN + k) * T + f;
+          const float2 e0 = spec[sp][fo + 1][k];
+          const float g0 = unit_gain ? 1.f : gain[sp][fo + 1];
+          const float2 v0 = poison ? make_float2(qnan, qnan) : make_float2(g0 * e0.x, g0 * e0.y);
+          if (n == 2) {
+            const float2 e1 = spec[sp][fo + 2][k];
+            const float g1 = unit_gain ? 1.f : gain[sp][fo + 2];
+            const float2 v1 = poison ? make_float2(qnan, qnan) : make_float2(g1 * e1.x, g1 * e1.y);
+            st_out(reinterpret_cast<float4*>(a.est_out + o), make_float4(v0.x, v0.y, v1.x, v1.y));
+          } else {
+            st_out(a.est_out + o, v0);
+          }
+        }
+      }
+      return;
+    }
     constexpr int NI = (2 * NBIN * IP_OWN + 511) / 512;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -302,9 +335,59 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   lds_sync();  // every frame's time samples in place for the overlap-add
   stamp(4);
   // 3) overlap-add of the owned segments, times the reciprocal window envelope (torch.istft)
+  const int nseg = min(IP_OWN, T - f0) + ((f0 + IP_OWN >= T) ? 1 : 0);
+  if (a.N % 4 == 0) {
+    // four consecutive samples per lane (16-B LDS reads and stores: a quarter of the store instructions), each sample's
+    // arithmetic as below (the same bits)
+    const int q4 = 4 * (tid & (HOP / 4 - 1));
+    float inv_mid[4], inv_last[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float w0 = a.window[q4 + e], w1 = a.window[q4 + e + HOP];
+      inv_mid[e] = 1.f / (w0 * w0 + w1 * w1);
+      inv_last[e] = 1.f / (w1 * w1);
+    }
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      float* yb = a.y + ((size_t)b * 2 + sp) * a.N;
+      for (int i = tid; i < nseg * (HOP / 4); i += 512) {
+        const int j = f0 + i / (HOP / 4);
+        const int n = j * HOP + q4 - HOP;
+        if (n < 0 || n >= a.N) continue;  // segment 0 lies in the centre padding
+        const float4 cur = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(spec[sp][j - fbeg]) + q4);
+        const float4 prv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(spec[sp][j - 1 - fbeg]) + q4 + HOP);
+        const float c4[4] = {cur.x, cur.y, cur.z, cur.w}, p4[4] = {prv.x, prv.y, prv.z, prv.w};
+        float o4[4];
+        if (j < T) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float num = 0.f;
+            num += c4[e];
+            num += p4[e];
+            o4[e] = poison ? qnan : num * inv_mid[e];
+          }
+        } else {  // segment T: frame T - 1 only
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float num = 0.f;
+            num += p4[e];
+            o4[e] = poison ? qnan : num * inv_last[e];
+          }
+        }
+        if (n + 3 < a.N) {
+          st_out(reinterpret_cast<float4*>(yb + n), make_float4(o4[0], o4[1], o4[2], o4[3]));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < a.N) st_out(yb + n + e, o4[e]);
+        }
+      }
+    }
+    stamp(5);
+    return;
+  }
   const int q = tid & (HOP - 1);  // this thread's sample phase in every segment
   const float wq0 = a.window[q], wq1 = a.window[q + HOP];
-  const int nseg = min(IP_OWN, T - f0) + ((f0 + IP_OWN >= T) ? 1 : 0);
   const float inv_mid = 1.f / (wq0 * wq0 + wq1 * wq1);  // segments 1..T-1: frame j and frame j-1
   const float inv_last = 1.f / (wq1 * wq1);             // segment T: frame T-1 only
 #pragma unroll
