@@ -51,6 +51,7 @@ struct PackedW {
   size_t wbf = 0, fbf = 0;  // bf16 bits of the row-scaled weight, row-major and in fragment order (PREC_BF16)
   size_t fl8 = 0;           // e4m3 lo plane in K-step-pair fragment order (bytes, stored in hblob; sepvad_internal.h WQ_*)
   size_t fi8 = 0;           // ... the same as int8 steps of 2^-WQ_LO_SHIFT, biased by 128
+  size_t fq = 0;            // the int8 lo plane's values (q * 2^-WQ_LO_SHIFT, exact) as fp16 in flo's order (two slices)
   size_t ff32 = 0;          // the row-scaled fp32 weight in the same fragment order (float blob; fused PREC_F32)
 };
 
@@ -158,6 +159,7 @@ struct sepvad_model {
   int tcn_cap_p[4] = {};        // ... per operand precision (PREC_*)
   __half* twf = nullptr;        // [nblk][WF_BLOCK] fragment-ordered fp16 hi/lo weights (F16X3, SEPVAD_WLO_F16)
   __half* twq[3] = {};          // [nblk][WQ_BLOCK] fragment-ordered fp16 hi + byte lo weights: [1] e4m3, [2] int8
+  __half* twfq = nullptr;       // [nblk][WF_BLOCK] as twf, the lo plane holding the int8 plane's values (two slices)
   int lo8 = 2;                  // k_tcn's weight lo plane: 0 fp16, 1 e4m3, 2 int8 (default); SEPVAD_WLO / sepvad_set_weight_lo
   int tcn_cap_q[3] = {};        // co-resident capacity of the byte-lo k_tcn variants
   int tcn2_cap_p[4] = {};       // ... of the two-slice (64-frame) k_tcn, per precision
@@ -280,6 +282,12 @@ namespace {
 // [cout][cin] fp32 -> zero-padded [mpad][cin] fp32 + the fp16 hi/lo split of each row scaled by
 // 2^-e (e chosen so the row's max |w| lands in [0.5, 1)); scale[m] = 2^(e + col_e) undoes it exactly, and
 // also the 2^-col_e the GEMM applies to its A operand before splitting it (range guard, see range_exp).
+// int8 step of a lo residual (|lo| <= 2^-12 -> |q| <= 128; +128, a tie at half an ulp of hi, saturates to 127)
+int lo_q(float lo) {
+  const double q = std::nearbyint(std::ldexp((double)lo, WQ_LO_SHIFT));
+  return (int)std::max(-128.0, std::min(127.0, q));
+}
+
 PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int cin, int mpad, int col_e = 0) {
   PackedW p;
   std::vector<float> w32((size_t)mpad * cin, 0.f), sc(mpad, 1.f);
@@ -315,7 +323,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
   // B operand): [mpad/32 row tiles][cin/16 K steps][64 lanes][8 halves], lane l -> row 32*mt + (l & 31),
   // k = 16*s + 8*(l >> 5) + j.
   if (mpad % 32 == 0 && cin % 16 == 0) {
-    std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin), fb((size_t)mpad * cin);
+    std::vector<__half> fh((size_t)mpad * cin), fl((size_t)mpad * cin), fb((size_t)mpad * cin), fqv((size_t)mpad * cin);
     std::vector<float> ff((size_t)mpad * cin);
     size_t q = 0;
     for (int mt = 0; mt < mpad / 32; ++mt)
@@ -326,6 +334,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
             fh[q] = hi[src];
             fl[q] = lo[src];
             fb[q] = bf[src];
+            fqv[q] = __float2half_rn(std::ldexp((float)lo_q(lo32[src]), -WQ_LO_SHIFT));  // exact in fp16
             // exact: a power-of-two row scale (PREC_F32: v_mfma_f32_32x32x2_f32 pairs k = 8 h + j, tcn_kernel.h)
             ff[q] = w32[src] * srow[src / cin];
           }
@@ -333,6 +342,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
     p.fhi = pk.addh(fh);
     p.flo = pk.addh(fl);
     p.fbf = pk.addh(fb);
+    p.fq = pk.addh(fqv);
     // e4m3 lo plane: lane l, K-step pair pr -> 16 bytes: j = 0..7 of step 2 pr, then of step 2 pr + 1
     if ((cin / 16) % 2 == 0) {
       std::vector<uint8_t> f8((size_t)mpad * cin), i8((size_t)mpad * cin);
@@ -345,8 +355,7 @@ PackedW pack_pointwise(Packer& pk, const std::vector<float>& w, int cout, int ci
                 const size_t src = (size_t)(32 * mt + (l & 31)) * cin + 16 * (2 * pr + h) + 8 * (l >> 5) + j;
                 f8[b] = e4m3_rn(lo32[src] * (float)(1 << WQ_LO_SHIFT));  // exact power-of-two scaling
                 // int8: |lo| <= 2^-12 -> |q| <= 128; +128 (a tie at half an ulp of hi) saturates to 127
-                const double q = std::nearbyint(std::ldexp((double)lo32[src], WQ_LO_SHIFT));
-                i8[b] = (uint8_t)(std::max(-128.0, std::min(127.0, q)) + 128.0);
+                i8[b] = (uint8_t)(lo_q(lo32[src]) + 128);
               }
       std::vector<__half> f8h(f8.size() / 2);
       std::memcpy(f8h.data(), f8.data(), f8.size());
@@ -502,7 +511,7 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   h->gran_slots = h->tcn_cap;
   for (int p : {PREC_F16X3, PREC_F16, PREC_BF16}) h->gran_slots = std::max(h->gran_slots, 2 * h->tcn2_cap_p[p]);
   for (int q = 1; q <= 2; ++q) h->gran_slots = std::max(h->gran_slots, 2 * h->tcn2_cap_q[q]);
-  std::vector<__half> wf(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
+  std::vector<__half> wf(WF_BLOCK * h->nblk), wfq(WF_BLOCK * h->nblk), ws16(WS_BLOCK * h->nblk), wsbf(WS_BLOCK * h->nblk), wq(WQ_BLOCK * h->nblk), wi(WQ_BLOCK * h->nblk);
   std::vector<float> pb((size_t)PB_SIZE * h->nblk, 0.f);
   std::vector<float> wf32(WS32_BLOCK / 2 * h->nblk);
   const bool rec = h->cfg.ln_mode == SEPVAD_LN_RECURSIVE, res = h->cfg.ln_mode == SEPVAD_LN_RESIDUAL;
@@ -513,6 +522,10 @@ int init_fused(sepvad_model* h, const Packer& pk) {
     std::copy_n(pk.hblob.begin() + bo.w1.flo, WF_W1L, w + WF_W1L);
     std::copy_n(pk.hblob.begin() + bo.w2.fhi, WF_W2L - WF_W2H, w + WF_W2H);
     std::copy_n(pk.hblob.begin() + bo.w2.flo, WF_W2L - WF_W2H, w + WF_W2L);
+    __half* wqf = wfq.data() + WF_BLOCK * i;
+    std::copy_n(w, WF_BLOCK, wqf);
+    std::copy_n(pk.hblob.begin() + bo.w1.fq, WF_W1L, wqf + WF_W1L);
+    std::copy_n(pk.hblob.begin() + bo.w2.fq, WF_W2L - WF_W2H, wqf + WF_W2L);
     __half* wqb = wq.data() + WQ_BLOCK * i;
     std::copy_n(pk.hblob.begin() + bo.w1.fhi, WQ_W1L, wqb);
     std::copy_n(pk.hblob.begin() + bo.w1.fl8, WQ_W2H - WQ_W1L, wqb + WQ_W1L);
@@ -554,6 +567,8 @@ int init_fused(sepvad_model* h, const Packer& pk) {
   }
   HIPCHK(hipMalloc(&h->twf, wf.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twf, wf.data(), wf.size() * sizeof(__half), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->twfq, wfq.size() * sizeof(__half)));
+  HIPCHK(hipMemcpy(h->twfq, wfq.data(), wfq.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twq[1], wq.size() * sizeof(__half)));
   HIPCHK(hipMemcpy(h->twq[1], wq.data(), wq.size() * sizeof(__half), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->twq[2], wi.size() * sizeof(__half)));
@@ -1230,6 +1245,14 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     ta.hwh = h->prec == PREC_F32 ? reinterpret_cast<const __half*>(h->P(h->wout_spk.ff32))
                                  : h->H(h->prec == PREC_BF16 ? h->wout_spk.fbf : h->wout_spk.fhi);
     ta.hwl = h->H(ta.lo8 == 2 ? h->wout_spk.fi8 : (ta.lo8 == 1 ? h->wout_spk.fl8 : h->wout_spk.flo));
+    // two slices, int8 lo plane: the same lo values streamed as fp16 (no widening VALU beside the MFMAs; at two slices
+    // the weight stream is not the bound). Bitwise equal to the int8 kernel: its widening is exact (tcn_common.h
+    // lo8_widen), so both feed the MFMAs the same fp16 operands. SEPVAD_TCN_WQ16=0: the int8 kernel.
+    if (nsl == 2 && ta.lo8 == 2 && h->tcn2_cap_p[PREC_F16X3] >= cap && env_int("SEPVAD_TCN_WQ16", 1)) {
+      ta.lo8 = 0;
+      ta.wfrag = h->twfq;
+      ta.hwl = h->H(h->wout_spk.fq);
+    }
     ta.hwscale = h->P(h->wout_spk.scale); ta.hbias = h->P(h->bo_spk);
     ta.hnyw = h->P(h->out_nyw); ta.hnyb = h->P(h->out_nyb);
     if (vad_in_head) {
@@ -1933,6 +1956,7 @@ void sepvad_destroy(sepvad_handle h) {
   if (h->fork) (void)hipEventDestroy(h->fork);
   for (auto& c : h->ctx) free_ctx(c.release());
   if (h->twf) (void)hipFree(h->twf);
+  if (h->twfq) (void)hipFree(h->twfq);
   for (__half* q : h->twq)
     if (q) (void)hipFree(q);
   if (h->twf16) (void)hipFree(h->twf16);

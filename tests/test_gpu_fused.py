@@ -177,6 +177,21 @@ def test_two_slices_bitwise_equal_one_slice(cname, N, nets, monkeypatch):
     assert torch.equal(s1, s2) and torch.equal(v1, v2) and torch.equal(e1, e2)
 
 
+@pytest.mark.parametrize("N", [32000, 130816])
+def test_two_slices_int8_and_fp16_lo_planes_bitwise(N, nets, monkeypatch):
+    """Two-slice workgroups stream the int8 lo plane's values as fp16 (api.hip twfq: no widening VALU beside the MFMAs);
+    SEPVAD_TCN_WQ16=0 streams the int8 bytes and widens them in registers (exact). Same MFMA operands: equal bits."""
+    from sep_tfanet_vad_amd import synth
+    x = torch.from_numpy(synth.make_batch(3, N, 4242)[0]).to(DEV)
+    net = nets["with_vad"]
+    monkeypatch.setenv("SEPVAD_TCN_WQ16", "0")
+    si, vi, ei, ui = _run_slices(net, x, 2, monkeypatch)
+    monkeypatch.setenv("SEPVAD_TCN_WQ16", "1")
+    sf, vf, ef, uf = _run_slices(net, x, 2, monkeypatch)
+    assert (ui, uf) == (2, 2)
+    assert torch.equal(si, sf) and torch.equal(vi, vf) and torch.equal(ei, ef)
+
+
 @pytest.mark.parametrize("prec", ["bf16", "f16"])
 def test_two_slices_reduced_precision_arms(prec, nets, monkeypatch):
     """The single-product arms (BASELINE cfg 2 bf16, cfg 5 fp16) on two-slice workgroups: bitwise the one-slice
