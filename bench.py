@@ -91,16 +91,17 @@ RING_FILE = "r02bi_ring_gemm.txt"       # GEMM-phase stream floor per CU (tools/
 STREAM_FLOOR_GBPS = 103.2
 
 
-def weight_stream(B, T, precision, avg_launch_s, n_cu=256, wlo="f16"):
-    """The fused TCN's per-CU weight stream: every workgroup pulls every block's weights once per 32-frame
-    slice it owns, so each CU moves slices x 24 x (256x256 + 512x256) x 4 (fp16 hi/lo) or 2
-    bytes per launch. With the texture-path busy fraction from the committed counters where they apply."""
+def weight_stream(B, T, precision, avg_launch_s, n_cu=256, wlo="f16", nsl=1):
+    """The fused TCN's per-CU weight stream: every workgroup pulls every block's weights once per utterance it
+    runs, for its nsl 32-frame slices together, so each CU moves rounds x 24 x (256x256 + 512x256)
+    x 4 (fp16 hi/lo), 3 (byte lo plane) or 2 bytes per launch. With the texture-path busy fraction from the committed
+    counters where they apply."""
     G = (T + 31) // 32
-    slices = -(-B * G // n_cu)
+    slices = -(-B * (G // nsl) // n_cu)
     wbytes = weight_bytes(precision, wlo)
     per_cu = slices * 24 * (256 * 256 + 256 * 512) * wbytes
     rate = per_cu / avg_launch_s / 1e9
-    out = {"bytes_per_cu_per_launch": per_cu, "slices_per_cu": slices, "achieved_GBps_per_cu": round(rate, 2),
+    out = {"bytes_per_cu_per_launch": per_cu, "workgroup_rounds": slices, "slices_per_workgroup": nsl, "achieved_GBps_per_cu": round(rate, 2),
            # the same two GEMMs streamed back to back with nothing else (tools/probe_src/ring_gemm.hip)
            "floor_GBps_per_cu": STREAM_FLOOR_GBPS, "frac_of_floor": round(rate / STREAM_FLOOR_GBPS, 3),
            "floor_source": "profiles/" + RING_FILE, "ta_busy_frac": None, "ta_source": None}
@@ -451,6 +452,11 @@ def main():
         n_res += tm["res_out_launches"]; n_gemm += tm["gemm_launches"]
     h.set_timing(False)
     fused = h.fused_status()  # synchronises; raises if a fused hand-off gave up
+    # two-slice launches stream the int8 lo plane's values as fp16 (api.hip twfq, SEPVAD_TCN_WQ16): 4 bytes per weight
+    wlo_streamed, nsl = args.wlo, (h.fused_slices() if fused else 1)
+    if fused and args.precision == "f16x3" and args.wlo == "i8" and nsl == 2 \
+            and os.environ.get("SEPVAD_TCN_WQ16", "1") != "0":
+        wlo_streamed = "f16"
 
     if rank == 0:
         total_utt = world * B * args.steps
@@ -458,7 +464,7 @@ def main():
         res_avg_s = res_ms / n_res / 1e3
         if fused:
             # dominant kernel = the fused persistent TCN (all 24 blocks in one launch)
-            flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision, args.wlo)
+            flops_launch, bytes_launch = tcn_flops(B, T, args.precision), tcn_bytes(B, T, args.precision, wlo_streamed)
             body = ("k_tcn<LD_RECURSIVE> (fused persistent TCN: 24 x [conv1d 256->256, depthwise conv, res_out "
                     "512->256, TF-attention, recursive LN] + output head 256->514 and VAD conv1_1 taps, ")
             if args.precision == "f16x3":
@@ -512,7 +518,9 @@ def main():
             # (v_mfma_f32_32x32x2_f32), or the reduced arm's operand; everything outside the GEMMs is fp32
             "dtype": {"f16x3": "f16x3 (fp32-accurate)", "fp32": "fp32", "bf16": "bf16", "f16": "f16"}[args.precision],
             "ieee_fp32": args.precision == "fp32",
-            "gemm_arithmetic": args.precision + (f" (weight lo plane {args.wlo})" if args.precision == "f16x3" else ""),
+            "gemm_arithmetic": args.precision + (f" (weight lo plane {args.wlo}"
+                                                 + (", streamed as fp16" if wlo_streamed != args.wlo else "") + ")"
+                                                 if args.precision == "f16x3" else ""),
             "split": args.split,
             "schedule": "fused" if fused else "multi-kernel",
             "data": "synthetic: seeded PCG64 2-speaker mixtures (0 dB SIR, noise SNR U[0,15] dB) and PCG64 "
@@ -548,7 +556,7 @@ def main():
             },
         }
         if fused:
-            out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s, wlo=args.wlo)
+            out["roofline"]["weight_stream"] = weight_stream(B, T, args.precision, res_avg_s, wlo=wlo_streamed, nsl=nsl)
             if args.precision == "f16x3" and args.wlo == PMC_WLO and B == B_PER_GPU and N == N_SAMPLES:
                 out["roofline"]["caches"] = cache_counters(args.wlo)
             # the same fraction from the committed rocprofv3 average of the kernel (headline configuration only)
