@@ -48,8 +48,7 @@ __global__ __launch_bounds__(PIT_THREADS) void k_pit_l1_partial(PitArgs a) {
 // staged in LDS by all threads (every load in flight at once), then thread j < 4 adds value j of the blocks in block
 // order, loads 8 at a time -- the same order and bits as one thread walking the partials (which took ~66 us for the
 // 512 blocks of a 16 k-sample overlap: one dependent global load per add).
-__global__ __launch_bounds__(256) void k_pit_l1_sums(PitArgs a, int nblk, double* sums) {
-  __shared__ double part[PIT_MAX_BLOCKS * 4];
+__device__ __forceinline__ void pit_block_sums(const PitArgs& a, int nblk, double* part, double* sums) {
   for (int i = threadIdx.x; i < nblk * 4; i += 256) part[i] = a.partial[i];
   __syncthreads();
   if (threadIdx.x >= 4) return;
@@ -67,11 +66,16 @@ __global__ __launch_bounds__(256) void k_pit_l1_sums(PitArgs a, int nblk, double
   sums[j] = pw;
 }
 
+__global__ __launch_bounds__(256) void k_pit_l1_sums(PitArgs a, int nblk, double* sums) {
+  __shared__ double part[PIT_MAX_BLOCKS * 4];
+  pit_block_sums(a, nblk, part, sums);
+}
+
 // One block: pairwise means from the sums (of this device's rows, or all-reduced over the ranks of a
 // sharded stream batch: nn.L1Loss means over the WHOLE batch, model/pit_wrapper.py:172-177), the permutation
 // loss set (einsum over one-hot perms / n_src, :289-300), torch.min's first-minimum choice (:308), the
 // indices (:311) for this device's a.B rows.
-__global__ __launch_bounds__(256) void k_pit_l1_choose(PitArgs a, const double* sums, double cnt) {
+__device__ __forceinline__ void pit_choose(const PitArgs& a, const double* sums, double cnt) {
   // every thread makes the same choice from the same sums; the per-row indices are written by all threads
   double pw[4];
   for (int j = 0; j < 4; ++j) pw[j] = sums[j];
@@ -93,6 +97,20 @@ __global__ __launch_bounds__(256) void k_pit_l1_choose(PitArgs a, const double* 
     for (int j = 0; j < 4; ++j) a.pw_out[j] = m[j];
 }
 
+__global__ __launch_bounds__(256) void k_pit_l1_choose(PitArgs a, const double* sums, double cnt) {
+  pit_choose(a, sums, cnt);
+}
+
+// An unsharded batch: the block sums and the choice in one launch (the sums through LDS; also written to `sums`)
+__global__ __launch_bounds__(256) void k_pit_l1_sums_choose(PitArgs a, int nblk, double* sums, double cnt) {
+  __shared__ double part[PIT_MAX_BLOCKS * 4];
+  __shared__ double tot[4];
+  pit_block_sums(a, nblk, part, tot);
+  __syncthreads();
+  if (threadIdx.x < 4) sums[threadIdx.x] = tot[threadIdx.x];
+  pit_choose(a, tot, cnt);
+}
+
 hipError_t launch_pit_l1_sums(const PitArgs& a, double* sums, hipStream_t s) {
   if (a.B < 1 || a.L < 1 || a.nblk < 1 || a.nblk > PIT_MAX_BLOCKS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_pit_l1_partial, dim3(a.nblk), dim3(PIT_THREADS), 0, s, a);
@@ -108,9 +126,10 @@ hipError_t launch_pit_l1_choose(const PitArgs& a, const double* sums, double cou
 hipError_t launch_pit_l1(const PitArgs& a, hipStream_t s) {
   // the sums live in the scratch right after the block partials
   double* sums = a.partial + (size_t)PIT_MAX_BLOCKS * 4;
-  hipError_t e = launch_pit_l1_sums(a, sums, s);
-  if (e != hipSuccess) return e;
-  return launch_pit_l1_choose(a, sums, (double)a.B * (double)a.L, s);
+  if (a.B < 1 || a.L < 1 || a.nblk < 1 || a.nblk > PIT_MAX_BLOCKS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pit_l1_partial, dim3(a.nblk), dim3(PIT_THREADS), 0, s, a);
+  hipLaunchKernelGGL(k_pit_l1_sums_choose, dim3(1), dim3(256), 0, s, a, a.nblk, sums, (double)a.B * (double)a.L);
+  return hipGetLastError();
 }
 
 // dst[b][i][d0 + n] = src[b][perm[b][i]][s0 + n], n < H  (perm null = identity)
