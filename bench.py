@@ -176,6 +176,10 @@ PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
 PMC_FILE_FUSED = "r05prof_pmc_tcn.json"     # fused schedule (k_tcn)
 PMC_WLO = "i8"                             # ... measured with this weight lo plane
 DEFAULT_SPLIT = 1
+# Default (timed steps, warmup steps) per workload: ~0.1 s of untimed load, then ~0.5 s timed. The shader clock ramps
+# during the first tens of milliseconds of load: 3 warmup steps and 20 timed ones (rounds 1-5) measured the ramp,
+# 122-124k utt/s at cfg 2 against 137-140k with 100+ warmup steps on the same box (profiles/r05_warm/lines.txt).
+STEADY_STEPS = {"offline": (1000, 200), "cfg4": (600, 120), "cfg5": (600, 120), "long": (600, 120), "stream": (40, 8)}
 
 
 def host_cores():
@@ -374,8 +378,10 @@ def bench_stream(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: about half a second of sustained load, STEADY_STEPS)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (default: about 0.1 s, STEADY_STEPS: the GPU's clocks ramp under load)")
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU per step (default: the workload's)")
     ap.add_argument("--samples", type=int, default=None)
     ap.add_argument("--split", type=int, default=DEFAULT_SPLIT,
@@ -395,6 +401,9 @@ def main():
                          "N=256000, T=1001: fused groups of 32 workgroups; --samples 480000 --batch 4 for 30 s files, groups of 59 "
                          "spanning XCDs); stream: cfg 3 streaming wrapper")
     args = ap.parse_args()
+    steps, warmup = STEADY_STEPS[args.workload]
+    args.steps = steps if args.steps is None else args.steps
+    args.warmup = warmup if args.warmup is None else args.warmup
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)

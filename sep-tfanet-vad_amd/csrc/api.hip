@@ -118,8 +118,6 @@ struct StreamCtx {
   int last_B = 0, last_N = 0;           // shape of the last forward on this stream (sepvad_side_outputs)
   long long seq = 0;                    // handle-wide id of the last forward on this stream (side outputs are tied to one)
   unsigned long long used = 0;          // LRU stamp (context cap, get_ctx)
-  hipEvent_t done = nullptr;            // recorded after every enqueue on this context: eviction waits on it (the
-                                        // caller's stream itself may already be destroyed by then)
 };
 
 }  // namespace
@@ -424,8 +422,6 @@ int ws_reserve(StreamCtx* c, int B, int N) {
   w.rec_gate = (double*)(base + oRg); w.rec_g1 = (double*)(base + oR1); w.rec_dw = (double*)(base + oRd);
   w.rec_mom = (double*)(base + oRm); w.rec_hs = (double*)(base + oRh); w.rec_vad = (double*)(base + oRv);
   w.vP = (float*)(base + oVp);
-  // the zeroing is this context's latest work: eviction (get_ctx) drains `done` before freeing the buffers
-  if (c->done) HIPCHK(hipEventRecord(c->done, (hipStream_t)c->stream));
   return SEPVAD_OK;
 }
 
@@ -585,7 +581,6 @@ int init_fused(sepvad_model* h, const Packer& pk) {
 }
 
 void free_ctx(StreamCtx* c) {
-  if (c->done) (void)hipEventDestroy(c->done);
   if (c->ws.base) (void)hipFree(c->ws.base);
   if (c->tgran) (void)hipFree(c->tgran);
   if (c->terr) (void)hipFree(c->terr);
@@ -605,13 +600,15 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
     size_t lru = 0;
     for (size_t i = 1; i < h->ctx.size(); ++i)
       if (h->ctx[i]->used < h->ctx[lru]->used) lru = i;
-    HIPCHK(hipEventSynchronize(h->ctx[lru]->done));  // its last enqueued work (not its stream: may be gone)
+    // every enqueued use of its buffers done: the whole device is drained, because the context's stream may already be
+    // destroyed with work pending (an event recorded after every forward cost each forward 5.8 us of queue time,
+    // profiles/r05_gap/; eviction is rare: more live streams than the cap)
+    HIPCHK(hipDeviceSynchronize());
     free_ctx(h->ctx[lru].release());
     h->ctx.erase(h->ctx.begin() + lru);
   }
   std::unique_ptr<StreamCtx, void (*)(StreamCtx*)> c(new StreamCtx(), free_ctx);
   c->stream = stream;
-  HIPCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   if (h->tcn_cap > 0) {
     const size_t gb = (size_t)h->gran_slots * 2 * NGR * sizeof(unsigned long long);
     HIPCHK(hipMalloc(&c->tgran, gb));
@@ -622,8 +619,6 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
   HIPCHK(hipHostMalloc((void**)&c->herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(c->herr, 0, 64);
   HIPCHK(hipHostGetDevicePointer((void**)&c->herr_dev, c->herr, 0));
-  // the async zeroing above is already enqueued work of this context: an eviction before its first forward drains it
-  HIPCHK(hipEventRecord(c->done, (hipStream_t)stream));
   if (h->res_B > 0) {
     const int rc = ws_reserve(c.get(), h->res_B, h->res_N);
     if (rc) return rc;
@@ -1537,7 +1532,6 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
   if (nsplit == 1) {
     if (ev_record(h, s)) return SEPVAD_E_HIP;
     rc = enqueue_chunk(h, cx, x, ldx, 0, B, N, out, kw, s, h->timing || h->probe_blk >= 0 ? &tr : nullptr, xm);
-    HIPCHK(hipEventRecord(cx->done, s));  // (also after a failed enqueue: whatever it queued)
     if (rc) return rc;
     if (ev_record(h, s)) return SEPVAD_E_HIP;
   } else {
@@ -1550,13 +1544,9 @@ int forward_impl(sepvad_model* h, const float* x, int ldx, int B, int N, const S
       rc = enqueue_chunk(h, cx, x, ldx, b0, bc, N, out, kw, h->sub[k], nullptr, xm);
       HIPCHK(hipEventRecord(h->join[k], h->sub[k]));
       HIPCHK(hipStreamWaitEvent(s, h->join[k], 0));
-      if (rc) {
-        HIPCHK(hipEventRecord(cx->done, s));
-        return rc;
-      }
+      if (rc) return rc;
       b0 += bc;
     }
-    HIPCHK(hipEventRecord(cx->done, s));
   }
   if (h->timing) {
     HIPCHK(hipEventSynchronize(h->ev.back()));
@@ -1756,7 +1746,6 @@ int side_outputs_locked(sepvad_model* h, const SepVadOutputs* out, void* stream)
     m.B = B; m.T = T; m.Tp = Tp; m.masks = w.masks; m.masks_b = out->masks_b; m.mask = out->mask;
     HIPCHK(launch_mask_side(m, s));
   }
-  HIPCHK(hipEventRecord(cx->done, s));
   return SEPVAD_OK;
 }
 }  // namespace
@@ -1784,7 +1773,6 @@ int32_t sepvad_stft_gate_test(sepvad_handle h, const float* x, int32_t B, int32_
   sa.activity = h->cfg.activity_input; sa.gate_w = h->P(h->gate);
   sa.S0 = w.S0; sa.gate_rec = w.rec_gate;
   HIPCHK(launch_stft_gate(sa, (hipStream_t)stream));
-  HIPCHK(hipEventRecord(cx->done, (hipStream_t)stream));
   return SEPVAD_OK;
 }
 

@@ -71,6 +71,30 @@ def test_two_streams_concurrently_match_serial(net):
     assert not bad, "\n".join(bad)
 
 
+def test_stream_context_eviction_matches_serial(net, monkeypatch):
+    """More live streams than the per-handle context cap (SEPVAD_MAX_STREAM_CTX=2): each new stream's context evicts the
+    least recently used one while forwards on the other streams are still queued (the eviction drains the device before
+    freeing the evicted workspace). Every output equals the serial forward's."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(24, 32000, 31)[0]).to(DEV)
+    with torch.no_grad():
+        ref = h.forward(x)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("SEPVAD_MAX_STREAM_CTX", "2")
+    streams = [torch.cuda.Stream() for _ in range(5)]
+    outs = []
+    for _ in range(2):
+        for st in streams:
+            with torch.cuda.stream(st):
+                outs.append(h.forward(x))
+    torch.cuda.synchronize()
+    assert h.fused_status()
+    for i, o in enumerate(outs):
+        for k in ("sep", "vad", "est"):
+            assert torch.equal(o[k], ref[k]), f"forward {i} {k}"
+
+
 def test_giveup_is_reported_once_and_not_sticky(net):
     g = load_golden("with_vad", "small")
     x = torch.from_numpy(g["x"]).to(DEV)

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=${1:-r05prof}
 out=gpurun_out/$tag
 mkdir -p $out
-bench="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline"
+bench="python3 bench.py --no-cpu-baseline"  # default steps: steady-state clocks (bench.py STEADY_STEPS)
 short="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 K="k_tcn<2, 1, false, 2, false, false, 1>"
 step() { echo "== $1 $(date +%T)"; }
