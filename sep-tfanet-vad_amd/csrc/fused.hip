@@ -11,6 +11,7 @@ namespace sepvad {
 namespace sepvad {
 template __global__ void k_tcn<LD_RECURSIVE, PREC_F16X3, false, 2, false, false, 2>(TcnArgs);
 template __global__ void k_tcn<LD_RECURSIVE, PREC_F16X3, false, 2, false, false, 1>(TcnArgs);
+template __global__ void k_tcn<LD_RECURSIVE, PREC_F16X3, false, 0, false, false, 2>(TcnArgs);
 template __global__ void k_tcn<LD_RECURSIVE, PREC_F32, false, 0, false, false, 1>(TcnArgs);
 #else
 // defined in fused_inst.hip, one explicit specialisation per object
