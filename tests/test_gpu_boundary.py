@@ -263,6 +263,20 @@ def test_side_attributes_materialised_on_read(net):
     assert net.spectrum == "user value"
 
 
+@pytest.mark.parametrize("N", [32000, 31900, 32002, 20001])
+def test_side_outputs_leave_outputs_bitwise(net, N):
+    """k_istft_pair writes est in paired 16-byte stores and overlap-adds in float4 when only est is asked for (even T,
+    N % 4 == 0) and frame by frame otherwise (side outputs on, odd T, ragged N): the same products in the same order, so
+    sep, vad and est are bitwise equal with and without the side outputs."""
+    from sep_tfanet_vad_amd import synth
+    h = net.native_handle(DEV)
+    x = torch.from_numpy(synth.make_batch(6, N, 77 + N)[0]).to(DEV)
+    plain = h.forward(x)
+    aux = h.forward(x, return_aux=True)
+    for k in ("sep", "vad", "est"):
+        assert torch.equal(plain[k], aux[k]), k
+
+
 def test_profiler_range_around_forward():
     """SURVEY §5 tracing: a torch.profiler range around the native forward when a profiler is active."""
     import sep_tfanet_vad_amd as pkg
