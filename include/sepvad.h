@@ -293,6 +293,10 @@ int32_t sepvad_timing(sepvad_handle h, double* gemm_ms, int32_t* gemm_launches, 
 void sepvad_destroy(sepvad_handle h);
 const char* sepvad_last_error(void);
 int32_t sepvad_abi_version(void);
+/* Source hash of this build: the first 16 hex digits of sha256 over include/sepvad.h and the library's sources
+ * (sep-tfanet-vad_amd/buildid.py, computed at build time). A static string; tests compare it with the hash of the
+ * tree they run in. No reference equivalent (build provenance). */
+const char* sepvad_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include "build/build_id.h"  // SEPVAD_BUILD_ID (Makefile: buildid.py)
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -685,6 +687,7 @@ extern "C" {
 
 const char* sepvad_last_error(void) { return g_err.c_str(); }
 int32_t sepvad_abi_version(void) { return SEPVAD_ABI_VERSION; }
+const char* sepvad_build_id(void) { return SEPVAD_BUILD_ID; }
 
 sepvad_handle sepvad_create(const SepVadConfig* cfg, const float* const* tensors, const char* const* names,
                             const int64_t* numels, int32_t n, int32_t device) {

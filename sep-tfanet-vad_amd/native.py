@@ -34,7 +34,19 @@ EXPORTED_SYMBOLS = (
     "sepvad_resample_filter", "sepvad_resample", "sepvad_normalize", "sepvad_si_sdr", "sepvad_vad_accuracy",
     "sepvad_rir_generate",
     "sepvad_set_timing", "sepvad_timing", "sepvad_destroy", "sepvad_last_error", "sepvad_abi_version",
+    "sepvad_build_id",
 )
+
+
+def build_id() -> str:
+    """Source hash the loaded library was built from (sepvad_build_id, include/sepvad.h)."""
+    return load_library().sepvad_build_id().decode()
+
+
+def tree_build_id() -> str:
+    """The same hash computed from this tree's sources (buildid.py)."""
+    from . import buildid
+    return buildid.source_hash()
 
 
 class SepVadConfig(ctypes.Structure):
@@ -151,6 +163,8 @@ def load_library(path: str = LIB_PATH):
     lib.sepvad_last_error.argtypes = []
     lib.sepvad_abi_version.restype = i32
     lib.sepvad_abi_version.argtypes = []
+    lib.sepvad_build_id.restype = ctypes.c_char_p
+    lib.sepvad_build_id.argtypes = []
     _lib = lib
     return lib
 

@@ -3,6 +3,8 @@
 Gates: separated waveforms max-abs <= 1e-4 (fp32 path); thresholded VAD labels
 bit-exact; SI-SDR within 0.01 dB. Kernel-level checks compare against plain PyTorch fp32 ops.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -52,6 +54,9 @@ def test_native_library_is_loaded():
     from sep_tfanet_vad_amd import native
     lib = native.load_library()
     assert lib.sepvad_abi_version() == 1
+    if not os.environ.get("SEPVAD_LIB"):  # the tested binary is built from this tree's sources
+        assert native.build_id() == native.tree_build_id(), (native.build_id(), native.tree_build_id())
+    print(f"libsepvad build id {native.build_id()}")
     assert torch.cuda.is_available()
 
 

@@ -70,6 +70,14 @@ def test_library_exports_every_header_symbol():
     assert lib.sepvad_abi_version() == 1
 
 
+def test_library_is_built_from_this_tree():
+    """The loaded library's source hash (sepvad_build_id) equals the hash of this tree's sources (buildid.py)."""
+    from sep_tfanet_vad_amd import native
+    if os.environ.get("SEPVAD_LIB"):
+        pytest.skip("SEPVAD_LIB: an alternative build on purpose")
+    assert native.build_id() == native.tree_build_id()
+
+
 def test_library_rejects_bad_config_without_gpu():
     from sep_tfanet_vad_amd import native
     lib = native.load_library()

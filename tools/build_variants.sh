@@ -1,21 +1,21 @@
 # Build A/B variants of libsepvad.so that differ only in compile-time switches of the fused TCN (tcn_kernel.h) for the
 # production combination (fp16x3, int8 lo plane: build/fused_x3l2.o); every other object is the tree's own.
-# usage: bash tools/build_variants.sh name1="-DTCN_X=0" name2="-DTCN_Y=0 -DTCN_Z=0" ...   -> var/lib_<name>.so
+# usage: bash tools/build_variants.sh name1="-DTCN_X=0" name2="-DTCN_Y=0 -DTCN_Z=0" ...   -> abl/lib_<name>.so
 set -e
 cd "$(dirname "$0")/.."
 make -s -C sep-tfanet-vad_amd/csrc ARCH=gfx950
-mkdir -p var
+mkdir -p abl
 objs=$(ls sep-tfanet-vad_amd/csrc/build/*.o | grep -v '/fused_x3l2.o$')
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-variable -mllvm -disable-promote-alloca-to-lds $flags \
-      -DFI_PRE=PREC_F16X3 -DFI_LQ=2 -c sep-tfanet-vad_amd/csrc/fused_inst.hip -o var/fused_$name.o &
+      -DFI_PRE=PREC_F16X3 -DFI_LQ=2 -c sep-tfanet-vad_amd/csrc/fused_inst.hip -o abl/fused_$name.o &
 done
 wait
 for spec in "$@"; do
   name=${spec%%=*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/lib_$name.so var/fused_$name.o $objs \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abl/lib_$name.so abl/fused_$name.o $objs \
       -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
-  rm -f var/fused_$name.o
+  rm -f abl/fused_$name.o
 done
-ls -la var/
+ls -la abl/
