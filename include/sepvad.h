@@ -182,7 +182,8 @@ int32_t sepvad_tcn_clock(sepvad_handle h, uint64_t* out, int32_t max_records, in
 
 /* Synchronises `stream` and frees the per-stream context (workspace, hand-off words, pinned give-up word) the handle
  * holds for it. Contexts are otherwise kept (at most SEPVAD_MAX_STREAM_CTX = 32 per handle by default, the least
- * recently used evicted after a device-wide sync: its stream may already be destroyed with work pending). */
+ * recently used evicted after a device-wide sync -- the host waits until every stream on the device is idle, other
+ * handles' and the application's work included -- because its stream may already be destroyed with work pending). */
 int32_t sepvad_release_stream(sepvad_handle h, void* stream);
 
 /* Kernel-level test entries of the forward's own front and back end (the fused schedule's k_stft_gate and

@@ -596,7 +596,8 @@ int get_ctx(sepvad_model* h, void* stream, StreamCtx** out) {
   for (auto& c : h->ctx)
     if (c->stream == stream) { c->used = ++h->use_clock; *out = c.get(); return SEPVAD_OK; }
   // cap the per-stream contexts (each holds a workspace, hand-off words and pinned memory): evict the least
-  // recently used one after draining its stream (SEPVAD_MAX_STREAM_CTX, default 32)
+  // recently used one after draining the whole device (SEPVAD_MAX_STREAM_CTX, default 32; include/sepvad.h notes the
+  // device-wide stall)
   const size_t cap = (size_t)std::max(1, env_int("SEPVAD_MAX_STREAM_CTX", 32));
   while (h->ctx.size() >= cap) {
     size_t lru = 0;
@@ -665,7 +666,8 @@ int check_giveup(StreamCtx* c) {
               w[1] & ((1u << TCN_EPOCH_BITS) - 1), w[2], w[3], w[3] / NGR, w[3] % NGR);
     // reported: clear the diagnostic words (the first timed-out poller sets them by a compare-and-swap from 0), so a
     // later give-up on this context reports its own wait, not this one's
-    (void)hipMemsetAsync(c->terr + 1, 0, 3 * sizeof(unsigned), (hipStream_t)c->stream);
+    // (synchronous, not on c->stream: a cached context's caller stream may already be destroyed)
+    (void)hipMemset(c->terr + 1, 0, 3 * sizeof(unsigned));
   }
   if (c->pending != 0) {
     c->pending = 0;
@@ -1246,7 +1248,10 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     // two slices, int8 lo plane: the same lo values streamed as fp16 (no widening VALU beside the MFMAs; at two slices
     // the weight stream is not the bound). Bitwise equal to the int8 kernel: its widening is exact (tcn_common.h
     // lo8_widen), so both feed the MFMAs the same fp16 operands. SEPVAD_TCN_WQ16=0: the int8 kernel.
-    if (nsl == 2 && ta.lo8 == 2 && h->tcn2_cap_p[PREC_F16X3] >= cap && env_int("SEPVAD_TCN_WQ16", 1)) {
+    // SEPVAD_TCN_WQ16=2: one-slice launches too (A/B)
+    const int wq16 = env_int("SEPVAD_TCN_WQ16", 1);
+    if (ta.lo8 == 2 && ((nsl == 2 && wq16 >= 1 && h->tcn2_cap_p[PREC_F16X3] >= cap) ||
+                        (nsl == 1 && wq16 >= 2 && h->tcn_cap_p[PREC_F16X3] >= cap))) {
       ta.lo8 = 0;
       ta.wfrag = h->twfq;
       ta.hwl = h->H(h->wout_spk.fq);

@@ -94,7 +94,7 @@ constexpr int IP_FR = IP_OWN + 1;
 #endif
 __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   __shared__ float2 tw[256];
-  __shared__ float2 spec[2][IP_FR][NBIN + 1];  // est of the computed frames; transformed in place
+  __shared__ __attribute__((aligned(16))) float2 spec[2][IP_FR][NBIN + 1];  // (16-B aligned: float4 overlap-add reads)  // est of the computed frames; transformed in place
   __shared__ float yn[2][4][IP_FR + 6];   // GN'd VAD features, frames fbeg-3 .. fbeg+IP_FR+2
   __shared__ float vadv[2][IP_FR + 4];    // vad at frames fbeg-2 .. fbeg+IP_FR+1
   __shared__ float gain[2][IP_FR];
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   // side outputs of the owned frames, bin-major [bs][k][f] (IP_OWN consecutive frames per bin): est from the
   // rows, sigmoid(mask) recomputed from the masks (read again: side path only)
   auto side_outputs = [&](bool unit_gain) {
-    if (a.est_out && !a.mask_out && T % 2 == 0) {
+    if (a.est_out && !a.mask_out && T % 2 == 0 && ((uintptr_t)a.est_out & 15) == 0) {
       // the forward's est alone (T even: a row starts 16-B aligned): two frames per 16-B store where the pair is aligned
       // (frames f0 + fo, f0 + fo + 1 with f0 + fo even), the odd one out alone -- half the store instructions of one
       // frame per lane (the store phase is issue-bound: every workgroup of the round stores at once)
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(512, ISTFT_WAVES) void k_istft_pair(IstftArgs a) {
   stamp(4);
   // 3) overlap-add of the owned segments, times the reciprocal window envelope (torch.istft)
   const int nseg = min(IP_OWN, T - f0) + ((f0 + IP_OWN >= T) ? 1 : 0);
-  if (a.N % 4 == 0) {
+  if (a.N % 4 == 0 && ((uintptr_t)a.y & 15) == 0) {
     // four consecutive samples per lane (16-B LDS reads and stores: a quarter of the store instructions), each sample's
     // arithmetic as below (the same bits)
     const int q4 = 4 * (tid & (HOP / 4 - 1));

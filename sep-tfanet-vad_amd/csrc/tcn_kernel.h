@@ -56,6 +56,16 @@ namespace sepvad {
 // the GEMM waits for them): k_tcn -2.4 % shader cycles at cfg 2, bitwise equal (profiles/r05_prio/). 0 = round 4.
 #define TCN_PRIO 1
 #endif
+#ifndef TCN_WPIPE
+// 1 (round 6): the byte lo plane's widening one K step ahead (wave_gemm): -0.2 % k_tcn cycles at cfg 2, bitwise equal
+// (profiles/r06a/cyc.txt)
+#define TCN_WPIPE 1
+#endif
+#ifndef TCN_A1V
+// 1 (round 6): conv1d PReLU slope a1 in a VGPR, not readfirstlane'd (hipcc hoisted that into the GEMM's first K step,
+// whose vmcnt wait then also waited for the block-parameter loads): -0.5 % cycles, with TCN_WPIPE -0.7 %, bitwise equal
+#define TCN_A1V 1
+#endif
 #ifndef TCN_SUB
 #define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)
 #endif
@@ -256,6 +266,11 @@ __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ah
       if constexpr (X3) aL[k][t] = *reinterpret_cast<const f16x8*>(Alo + aoff + t * FR * LDA + 16 * k);
     }
   }
+  // TCN_WPIPE (byte lo plane): the widened lo fragment of step s+1 computed during step s, so no VALU sits between a
+  // step's first and second MFMA (the second one's B operand)
+  constexpr bool WP = L8 && TCN_WPIPE;
+  f16x8 blw;
+  if constexpr (WP) blw = lo8_widen<LQ>(rl[0], 0);
   auto step = [&](int s, int i, bool pf) {
     const int cur = s % (AD + 1), nxt = (s + AD) % (AD + 1);
     if (s + AD < NS) {
@@ -273,7 +288,8 @@ __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ah
     } else if constexpr (X3) {
       const f16x8 bh = __builtin_bit_cast(f16x8, rh[i]);
       f16x8 bl;
-      if constexpr (L8) bl = lo8_widen<LQ>(rl[i >> 1], i & 1);
+      if constexpr (WP) bl = blw;
+      else if constexpr (L8) bl = lo8_widen<LQ>(rl[i >> 1], i & 1);
       else bl = __builtin_bit_cast(f16x8, rl[i]);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -281,6 +297,9 @@ __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ah
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[t], 0, 0, 0);
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
+      }
+      if constexpr (WP) {
+        if (s + 1 < NS) blw = lo8_widen<LQ>(rl[((i + 1) % RD) >> 1], (i + 1) & 1);
       }
     } else if constexpr (PRE == PREC_F16) {
 #pragma unroll
@@ -639,7 +658,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       // the epilogue's per-channel values straight into registers (no LDS round trip, no barrier)
       const float* pgl = a.prm + (size_t)bi * PB_SIZE;
-      const float ws1 = pgl[PB_WS1 + m], b1 = pgl[PB_B1 + m], a1 = unif(pgl[PB_A1]);
+      // (TCN_A1V: a1 kept in a VGPR -- its readfirstlane was hoisted into the GEMM's first K step, where the wait for it
+      // (vmcnt) also waited for the parameter blob loads issued just before)
+      const float ws1 = pgl[PB_WS1 + m], b1 = pgl[PB_B1 + m], a1 = TCN_A1V ? pgl[PB_A1] : unif(pgl[PB_A1]);
       const unsigned e1 = ++ep, tag1 = a.tag0 + e1;
       // ================= conv1d 256->256 (model/model.py:132) + PReLU =================
       f32x16v acc[NSL];
@@ -1068,7 +1089,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int r = 0; r < 16 * NSL; r += 2) {
             const f32x2 g2 = *reinterpret_cast<const f32x2*>(sm.at + trow(r)) * afm;  // frames trow(r), trow(r)+1
-            const f32x2 x = f32x2{rv[r >> 4][r & 15], rv[r >> 4][(r & 15) + 1]} * g2;
+            f32x2 x = f32x2{rv[r >> 4][r & 15], rv[r >> 4][(r & 15) + 1]} * g2;
+            // LD_ADD (x' = o + r'): the gated product's only use is that add, and hipcc contracted the pair into an FMA in
+            // one of the one- / two-slice instantiations and not the other (1-ulp differences, tests/test_gpu_fused.py
+            // test_two_slices_bitwise_other_configs); materialised, both round r' first as the other LN modes do
+            if constexpr (LM == LD_ADD) asm volatile("" : "+v"(x));
             rv[r >> 4][r & 15] = x.x; rv[r >> 4][(r & 15) + 1] = x.y;
           }
         }

@@ -55,7 +55,7 @@ def check_vad_labels(vad, v_ref, band=1e-4, flips_per=1e-4, where=""):
     far_flips = int((lab != lref)[~near].sum())
     near_flips = int((lab != lref)[near].sum())
     n, nb = lab.size, int(near.sum())
-    allowed = max(1, int(n * flips_per))
+    allowed = int(n * flips_per)  # 0 below 10 000 labels: small tests must be bit-exact in the band too
     msg = f"{where} VAD labels: {n}, within {band:g} of 0.5: {nb}, flips there: {near_flips} (allowed {allowed})"
     print(msg)
     if os.environ.get("SEPVAD_VAD_LABEL_LOG"):  # archived per round under profiles/ (tools/gpu_round*.sh)

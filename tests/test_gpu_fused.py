@@ -177,6 +177,33 @@ def test_two_slices_bitwise_equal_one_slice(cname, N, nets, monkeypatch):
     assert torch.equal(s1, s2) and torch.equal(v1, v2) and torch.equal(e1, e2)
 
 
+@pytest.mark.parametrize("variant", ["no_tf_attention", "no_ln"])
+@pytest.mark.parametrize("N", [32000, 130816])
+def test_two_slices_bitwise_other_configs(variant, N, monkeypatch):
+    """Two-slice vs one-slice workgroups on configurations the shipped configs do not reach: without
+    TF-attention (model/model.py:345-346 skipped; the two-slice kernel keeps its gates in dead-H storage and skips the
+    gating multiply) and with neither recursive nor residual LN (o = o + r, model/model.py:351-352: the LD_ADD
+    instantiation) -- the reference constructor's defaults (model/model.py:362-366). Bitwise equal, and within the
+    waveform gate of the fp32 oracle on utterance 0 (VAD labels bit-exact)."""
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import synth
+    cfg = dict(config_of("with_vad"), tf_attention=False) if variant == "no_tf_attention" else \
+        dict(config_of("with_vad"), apply_recursive_ln=False, apply_residual_ln=False)
+    net = pkg.SeparationModel(**cfg)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_state_dict(cfg, 31).items()}, strict=True)
+    net = net.eval().to(DEV)
+    x = torch.from_numpy(synth.make_batch(3, N, 606 + N)[0]).to(DEV)
+    s1, v1, e1, u1 = _run_slices(net, x, 1, monkeypatch)
+    s2, v2, e2, u2 = _run_slices(net, x, 2, monkeypatch)
+    assert (u1, u2) == (1, 2)
+    assert torch.equal(s1, s2) and torch.equal(v1, v2) and torch.equal(e1, e2)
+    from oracle.torch_ref import OracleModel
+    om = OracleModel(cfg, {k: torch.from_numpy(v) for k, v in synth.make_state_dict(cfg, 31).items()}, torch.float32)
+    s_ref, v_ref, _ = om(x[:1].cpu())
+    assert np.abs(s1[:1].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
+    check_vad_labels(v1[:1].cpu().numpy(), v_ref.numpy())
+
+
 @pytest.mark.parametrize("N", [32000, 130816])
 def test_two_slices_int8_and_fp16_lo_planes_bitwise(N, nets, monkeypatch):
     """Two-slice workgroups stream the int8 lo plane's values as fp16 (api.hip twfq: no widening VALU beside the MFMAs);
@@ -314,6 +341,28 @@ def test_fp32_gemms_run_fused(cname, nets, state_dicts):
     s_ref, v_ref, _ = om(x[:2])
     assert np.abs(sf[:2].cpu().numpy() - s_ref.numpy()).max() <= SEP_TOL
     check_vad_labels(vf[:2].cpu().numpy(), v_ref.numpy())
+
+
+@pytest.mark.parametrize("N", [261888, 960000])
+def test_fp32_gemms_long_groups_fused(N, nets):
+    """The exact-fp32 arm on whole files: G = 32 and 118 members take the long-group instantiation
+    (k_tcn<PREC_F32, LG = true>: tree reductions, its own fp32 A-plane strides, VAD-tile placement and LN staging).
+    Fused, and within SCHED_TOL of the multi-kernel fp32 schedule (same fp32 products, other summation order), VAD
+    labels equal to the multi-kernel schedule's."""
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    net.native_precision = "fp32"
+    try:
+        x = torch.from_numpy(synth.make_batch(2, N, 717 + N % 991)[0]).to(DEV)
+        sf, vf, _, used = _run(net, x, True)
+        assert used, "the fused TCN did not run"
+        sm, vm, _, used_m = _run(net, x, False)
+        assert not used_m
+    finally:
+        net.native_precision = "f16x3"
+    assert (sf - sm).abs().max().item() <= SCHED_TOL
+    assert (vf - vm).abs().max().item() <= VAD_SCHED_TOL
+    check_vad_labels(vf.cpu().numpy(), vm.cpu().numpy())
 
 
 def test_handoff_protocols_bitwise_identical(nets):

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import config_of
+from conftest import config_of, load_golden
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -93,3 +93,47 @@ def test_cli_run_end_to_end(tmp_path, state_dicts):
     with torch.no_grad():
         s2, _, _ = net(inference.prepare_input(sr_in, a, DEV), dict(inference.DEFAULT_INFERENCE_KW))
     assert torch.equal(s2, sep)
+
+
+def test_cli_without_vad_defaults_end_to_end(tmp_path, monkeypatch, state_dicts):
+    """cfg 1 as the reference CLI runs it (only_inference.py:68-97,111-117): every argument at its default except the
+    mix -- `-c config_without_vad.json -r model_without_vad.pth`, online streaming on, 32-bit wavs, `-ikw {}` (the
+    defaults of :102-108) -- on an 8 kHz int16 wav: resample -> normalise -> online windows -> forward -> save, through
+    the residual-LN (without_vad) configuration. The saved separation equals the forward called directly on the
+    prepared input, bitwise; and the same CLI path on the reference's own 16 kHz cfg input reproduces the reference's
+    without_vad golden (tests/golden/golden_without_vad_cfg.npz) within the waveform gate."""
+    import json
+    from scipy.io import wavfile
+    import sep_tfanet_vad_amd as pkg
+    from sep_tfanet_vad_amd import inference, synth
+    monkeypatch.chdir(tmp_path)  # the CLI defaults are paths relative to the working directory
+    (tmp_path / "config_without_vad.json").write_text(
+        json.dumps({"arch": {"type": "SeparationModel", "args": config_of("without_vad")}}))
+    torch.save({"state_dict": state_dicts["without_vad"], "epoch": 1}, "model_without_vad.pth")
+    mix = synth.make_batch(1, 28000, 77)[0][0]
+    wavfile.write("mix8k.wav", 8000, (mix * 24000).astype(np.int16))
+    inference.main(["-pm", "mix8k.wav"])
+    out = tmp_path / "results_withoutvad"
+    for f in ("Mixed_0.wav", "Speaker_0.wav", "Speaker_1.wav"):
+        assert (out / f).exists(), f
+    assert (out / "online_results" / "online_signal0.wav").exists()
+    assert not (out / "estimated_vad_0.npy").exists()  # only_inference.py:96 (Path vs str: never saved)
+    net = pkg.SeparationModel(**config_of("without_vad"))
+    inference.load_checkpoint(net, "model_without_vad.pth")
+    net = net.to(DEV)
+    sr_in, a = wavfile.read("mix8k.wav")
+    x = inference.prepare_input(sr_in, a, DEV)
+    assert sr_in == 8000 and tuple(x.shape) == (1, 56000)  # resampled to 16 kHz
+    with torch.no_grad():
+        sep, _, _ = net(x, dict(inference.DEFAULT_INFERENCE_KW))
+    for spk in range(2):
+        sr, s = wavfile.read(str(out / f"Speaker_{spk}.wav"))
+        assert sr == 16000 and np.array_equal(s, sep[0, spk].cpu().numpy())
+    # the reference's cfg input (16 kHz, already in [-0.9, 0.9]) through the same CLI defaults
+    g = load_golden("without_vad", "cfg")
+    assert int(g["weights_seed"]) == 1234  # the state_dicts fixture's recipe seed
+    wavfile.write("golden16k.wav", 16000, g["x"][0].astype(np.float32))
+    inference.main(["-pm", "golden16k.wav", "-sp", "results_golden"])
+    for spk in range(2):
+        sr, s = wavfile.read(str(tmp_path / "results_golden" / f"Speaker_{spk}.wav"))
+        assert sr == 16000 and np.abs(s - g["sep"][0, spk]).max() <= 1e-4
