@@ -1267,6 +1267,14 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
     // diagnostics (SEPVAD_TCN_MAX_GROUPS): fewer groups per launch, so each loops over more utterances (tests reach
     // the epoch budget below with small batches)
     if (const int mg = env_int("SEPVAD_TCN_MAX_GROUPS", 0); mg > 0 && mg < ngroups) ngroups = mg;
+    // groups above 32 members (whole files, one slice): XCD runs (tcn_kernel.h RUN: R = ceil(G / 8) consecutive members
+    // per XCD, a group on 8 R blocks), where that costs this batch no group of the round; SEPVAD_TCN_RUNS=0: off
+    ta.run = 0;
+    if (nsl == 1 && G > 32 && env_int("SEPVAD_TCN_RUNS", 1)) {
+      const int R = (G + 7) / 8;
+      if (std::min(B, cap / (8 * R)) >= ngroups) ta.run = R;
+    }
+    const int gstride = ta.run ? 8 * ta.run : Gt;  // blocks per group
     // epochs per launch and group (tcn_kernel.h): 1 (XCD ids) + per utterance 4 per block with TF-attention (P1..P4;
     // 3 without) + 1 for the output head (P5). The tag is salt << TCN_EPOCH_BITS | epoch, so the last epoch of a
     // launch must stay below 2^TCN_EPOCH_BITS: an epoch carried into the salt bits would repeat the next launch's tags
@@ -1305,7 +1313,7 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         if (warm) {  // diagnostics: an unprobed launch first (warm caches)
           TcnArgs tw = ta;
           tw.probe = nullptr;
-          HIPCHK(launch_t(tw, ngl * Gt));
+          HIPCHK(launch_t(tw, ngl * gstride));
           ta.tag0 = (gsalt_lo + gsalt_n++) << TCN_EPOCH_BITS;
         }
       }
@@ -1319,19 +1327,19 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         HIPCHK(hipMemsetAsync(ta.clk, 0, 8 * sizeof(unsigned long long), s));
       }
       if (env_int("SEPVAD_TCN_INFO", 0))  // diagnostics: the persistent launch's shape
-        fprintf(stderr, "sepvad: k_tcn grid=%d G=%d slices=%d groups=%d B=%d capacity=%d\n", ngl * Gt, G, nsl, ngl, Bl,
-                cap);
-      const bool big = tcn_big(cap, Gt) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
+        fprintf(stderr, "sepvad: k_tcn grid=%d G=%d slices=%d groups=%d B=%d capacity=%d run=%d\n", ngl * gstride, G, nsl, ngl,
+                Bl, cap, ta.run);
+      const bool big = tcn_big(cap, gstride) && !env_int("SEPVAD_TCN_NO_ORDER", 0);
       TailProbe thp(h, s, "tcnhead");
       ta.hprobe = u0 == 0 ? thp.buf : nullptr;
       auto run = [&]() -> int {
         if (ev()) return SEPVAD_E_HIP;
-        HIPCHK(launch_t(ta, ngl * Gt));
+        HIPCHK(launch_t(ta, ngl * gstride));
         if (ev()) return SEPVAD_E_HIP;
         return SEPVAD_OK;
       };
       if (const int rc = big ? tcn_launch_ordered(h->device, s, run) : run()) return rc;
-      if (ta.hprobe) HIPCHK(thp.dump(ngl * Gt, 1));
+      if (ta.hprobe) HIPCHK(thp.dump(ngl * gstride, 1));
       if (tr) {
         tr->gemm_ev.push_back((int)h->ev.size() - 2);
         tr->g2_ev.push_back((int)h->ev.size() - 2);
@@ -1341,9 +1349,9 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipMemcpy(hp.data(), h->tprobe, probe_n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(probe_path, "wb")) {
-          const long long hdr[4] = {(long long)ngl * Gt, h->nblk, Gt, T};
+          const long long hdr[4] = {(long long)ngl * gstride, h->nblk, Gt, T};
           fwrite(hdr, sizeof(hdr), 1, f);
-          const size_t n0 = (size_t)ngl * Gt * h->nblk * 16;
+          const size_t n0 = (size_t)ngl * gstride * h->nblk * 16;
           fwrite(hp.data(), sizeof(unsigned long long), n0, f);
           fwrite(hp.data() + n0, sizeof(unsigned long long), n0 * 8, f);  // per-wave stamps (kernel layout)
           fclose(f);

@@ -20,9 +20,9 @@ template <int PRE, int LQ> int tcn_bpc_combo(int ln_mode, int nsl);
 
 hipError_t launch_tcn(const TcnArgs& a, int grid, hipStream_t s) {
   if (a.nsl != 1 && a.nsl != 2) return hipErrorInvalidValue;
-  const int gw = a.G / a.nsl;  // workgroups per group
+  const int gw = a.run > 0 ? 8 * a.run : a.G / a.nsl;  // blocks per group
   if (a.G < 1 || a.G > FG_MAX || a.G * FR < a.T || a.G * FR > a.Tp || a.G % a.nsl || grid < gw || grid % gw ||
-      (a.nsl == 2 && a.G > FG_WAVE))
+      (a.nsl == 2 && a.G > FG_WAVE) || (a.run > 0 && (a.nsl != 1 || a.G <= 32 || a.run != (a.G + 7) / 8)))
     return hipErrorInvalidValue;
   switch (a.prec) {
     case PREC_F16X3:

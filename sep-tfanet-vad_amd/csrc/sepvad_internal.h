@@ -323,6 +323,7 @@ constexpr int WQ_LO_SHIFT = 19;
 struct TcnArgs {
   int B, T, Tp, G, nblk, layer, ln_mode, tf_att, prec;
   int nsl;               // 32-frame slices (members) per workgroup: 1, or 2 (64 frames, G even and <= FG_WAVE)
+  int run;               // > 0: XCD runs of `run` = ceil(G / 8) consecutive members (G > 32, one slice), 8 run blocks per group
   int lo8;               // F16X3 weight lo plane: 0 fp16 (WF_* layout), 1 e4m3, 2 int8 (WQ_* layout)
   const __half* wfrag;   // [nblk][WF_BLOCK | WQ_BLOCK] (F16X3) or [nblk][WS_BLOCK] (F16 / BF16 bits) fragment-ordered weights
   const float* prm;      // [nblk][PB_SIZE] parameter blobs

@@ -465,8 +465,19 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // XCD (blocks b, b + 8, ...: round-robin dispatch), the remaining groups (fewer than 8) on consecutive blocks, which
   // span XCDs (their hand-offs write through; speed only). Those take the highest group ids: with u = grp, grp +
   // groups, ... they never take an extra utterance.
+  // RUN (a.run = R > 0, groups above 32 members, one slice): XCD runs -- member g on the blocks b with b % 8 = g / R,
+  // so R consecutive members share an XCD (round-robin dispatch: speed only, never correctness; the hand-off store
+  // types below are chosen from the members' XCD ids exchanged at epoch 1). A group spans 8 R blocks; the 8 R - G blocks
+  // past its last member exit at once. Without runs a long group's consecutive members sit on consecutive XCDs and
+  // every neighbour exchange (P1 halo rows, P3 frame sums) crosses XCDs.
+  const int RUN = LG ? a.run : 0;
   int grp, g;
-  {
+  if (RUN > 0) {
+    const int S = 8 * RUN, bb = (int)blockIdx.x % S;
+    grp = (int)blockIdx.x / S;
+    g = (bb & 7) * RUN + (bb >> 3);
+    if (g >= G) return;  // (before any publish or barrier: the whole workgroup leaves)
+  } else {
     const int na = (int)(gridDim.x / (8 * GW)) * 8 * GW;  // blocks of the XCD-aligned groups
     if ((int)blockIdx.x < na) {
       const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
@@ -477,7 +488,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       g = (int)blockIdx.x % GW;
     }
   }
-  const int ngroups = gridDim.x / GW;
+  const int ngroups = gridDim.x / (RUN > 0 ? 8 * RUN : GW);
   const int m0 = NSL * g;  // this workgroup's first member: slice s is member m0 + s
   // hand-off slots of this group: member mm, epoch e -> NGR words; tags a.tag0 + epoch
   u64* const gbase = a.gran + (size_t)grp * G * 2 * NGR;
@@ -510,6 +521,17 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // share an XCD (checked at epoch 1); the leaders' partials stay in L2 only when the whole group does (l2)
   const bool tree = LG && G > FG_TREE;
   bool sl2 = false;
+  // tree subgroups: leader k (k < nlead) is member lead_m(k); its subgroup is members sub_m(k, j), j < sub_n(k), in
+  // member order: members k, k + 8, ... (no runs) or the run k R .. k R + R - 1 (runs: the run shares an XCD)
+  const int nlead = RUN > 0 ? (G + RUN - 1) / RUN : 8;
+  auto lead_m = [&](int k) { return RUN > 0 ? k * RUN : k; };
+  auto sub_m = [&](int k, int j) { return RUN > 0 ? k * RUN + j : k + 8 * j; };
+  auto sub_n = [&](int k) { return RUN > 0 ? min(RUN, G - k * RUN) : (G - k + 7) / 8; };
+  const int myk = RUN > 0 ? g / RUN : g % 8;        // this member's subgroup
+  const bool leader = RUN > 0 ? g % RUN == 0 : g < 8;
+  // neighbour exchanges (P1 halo rows, P3 boundary frame sums) L2-only when the reading neighbour shares this XCD:
+  // l2p for the words member g - 1 reads, l2n for member g + 1's (long groups; the short ones use l2)
+  bool l2p = false, l2n = false;
   const int T = a.T, Tp = a.Tp, t0 = g * FW;
   const bool tf = a.tf_att != 0;
   // byte offset of this lane's 16-B fragment within its wave's weight stream (step 0)
@@ -583,7 +605,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       int same_t = 1, sub_t = 1;
       for (int mm = tid; mm < G; mm += NTHR) {
         same_t &= sm.gw[mm] == sm.gw[0];
-        if (LG) sub_t &= mm % 8 != g % 8 || sm.gw[mm] == sm.gw[g % 8];
+        if (LG) sub_t &= (RUN > 0 ? mm / RUN != myk : mm % 8 != myk) || sm.gw[mm] == sm.gw[lead_m(myk)];
       }
       const bool same = a.xmode == 0 && __syncthreads_and(same_t) != 0;
       const bool sub = a.xmode == 0 && (!LG || __syncthreads_and(sub_t) != 0);
@@ -591,6 +613,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // store a divergent branch, and at two slices hipcc spilled it and reloaded it behind vmcnt(0)
       l2 = __builtin_amdgcn_readfirstlane((int)same) != 0;
       sl2 = __builtin_amdgcn_readfirstlane((int)sub) != 0;
+      if constexpr (LG) {
+        const unsigned xg = sm.gw[g];
+        l2p = l2 || (a.xmode == 0 && (g == 0 || sm.gw[g - 1] == xg));
+        l2n = l2 || (a.xmode == 0 && (g + 1 >= G || sm.gw[g + 1] == xg));
+      } else {
+        l2p = l2n = l2;
+      }
       if (TP_ON && tid == 0 && a.nblk > 1) a.probe[((size_t)blockIdx.x * a.nblk + 1) * 16 + 15] = wall_clock64();
     }
     __syncthreads();  // staged LN records complete
@@ -701,9 +730,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
               for (int e = 0; e < 2; ++e) {
                 const float ve = e ? v.y : v.x;
                 // the workgroup's outer boundary rows only (the boundary between its own slices stays in H)
-                if (sl == 0 && r + e < 4 && hl == 0 && tl + e < dil) gputf(slot(m0, e1) + GW_TOP + (tl + e) * CH + m, tag1, ve, l2);
+                if (sl == 0 && r + e < 4 && hl == 0 && tl + e < dil) gputf(slot(m0, e1) + GW_TOP + (tl + e) * CH + m, tag1, ve, l2p);
                 if (sl == NSL - 1 && r + e >= 12 && hl == 1 && tl + e >= FW - dil)
-                  gputf(slot(m0 + NSL - 1, e1) + GW_BOT + (tl + e - (FW - dil)) * CH + m, tag1, ve, l2);
+                  gputf(slot(m0 + NSL - 1, e1) + GW_BOT + (tl + e - (FW - dil)) * CH + m, tag1, ve, l2n);
               }
             }
             st[2 * sl] = s0.x + s0.y;
@@ -943,7 +972,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int sl = 0; sl < 8; ++sl) s += sm.cs[tid][sl];
           sm.csum[tid] = s;
-          if (NSL == 1 || tid < 4 || tid >= FW - 4) gputf(slot(m0 + tid / FR, e3) + GW_COL + tid % FR, tag3, s, l2);
+          // (only the outer 4 frames each side: the neighbours' a_t inputs; the own frames stay in LDS)
+          if (tid < 4 || tid >= FW - 4) gputf(slot(m0 + tid / FR, e3) + GW_COL + tid % FR, tag3, s, tid < 4 ? l2p : l2n);
         }
         tcn_delay(g);  // diagnostics (SEPVAD_TCN_DELAY): member 0 late to its P2/P3 polls
       TPROBE(7);
@@ -964,20 +994,21 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           float s = 0.f, vat = 0.f;
           unsigned vq[FG_CHUNK] = {};
           if (tree) {
-            // level 1 (leaders g < 8): the row sums of members g, g + 8, ..., member order, published write-through
-            if (g < 8) {
+            // level 1 (the leaders): the row sums of their subgroup's members, member order, published for everyone
+            if (leader) {
               constexpr int L1 = 16;  // subgroup members polled per pass (a subgroup has <= 16 up to 128 members)
+              const int ns = sub_n(myk);
               float ss = 0.f;
-              for (int c0 = g; c0 < G; c0 += 8 * L1) {
+              for (int j0 = 0; j0 < ns; j0 += L1) {
                 const u64* p1[L1];
                 unsigned v1[L1];
 #pragma unroll
                 for (int mm = 0; mm < L1; ++mm)
-                  p1[mm] = (tid < CH && c0 + 8 * mm < G) ? slot(c0 + 8 * mm, e3) + GW_ROW + tid : nullptr;
+                  p1[mm] = (tid < CH && j0 + mm < ns) ? slot(sub_m(myk, j0 + mm), e3) + GW_ROW + tid : nullptr;
                 gpoll<L1>(p1, tag3, v1, a);
 #pragma unroll
                 for (int mm = 0; mm < L1; ++mm)
-                  if (c0 + 8 * mm < G) ss += __builtin_bit_cast(float, v1[mm]);
+                  if (j0 + mm < ns) ss += __builtin_bit_cast(float, v1[mm]);
               }
               if (tid < CH) gputf(slot(g, e3) + GW_SUB3 + tid, tag3, ss, l2);
             }
@@ -988,7 +1019,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           do {  // (level 2: one pass over the 8 leaders)
 #pragma unroll
             for (int mm = 0; mm < FG_CHUNK; ++mm) {
-              pp[mm] = tree ? (tid < CH ? slot(mm, e3) + GW_SUB3 + tid : nullptr)
+              pp[mm] = tree ? (tid < CH && mm < nlead ? slot(lead_m(mm), e3) + GW_SUB3 + tid : nullptr)
                             : ((tid < CH && c0 + mm < G) ? slot(c0 + mm, e3) + GW_ROW + tid : nullptr);
               tg[mm] = tag3;
             }
@@ -1010,7 +1041,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             if (tid < CH) {
 #pragma unroll
               for (int mm = 0; mm < FG_CHUNK; ++mm)
-                if (tree || c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
+                if (tree ? mm < nlead : c0 + mm < G) s += __builtin_bit_cast(float, v[mm]);
             }
             if (c0 == 0) {
               vat = __builtin_bit_cast(float, v[0]);
@@ -1145,13 +1176,13 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const unsigned e4 = ++ep, tag4 = a.tag0 + e4;
         if (tid < NSL * NMOM) gputd(slot(m0 + tid / NMOM, e4) + GW_P4 + 2 * (tid % NMOM), tag4, sm.dred[tid], tree ? sl2 : l2);
         if (tree) {
-          // level 1 (leaders g < 8): the records of members g, g + 8, ... (<= 16: one word per thread), summed in member
-          // order (double) by wave 0's lanes j < NMOM and published write-through
-          if (g < 8) {
-            const int nsub = (G - g + 7) / 8, nw = 2 * NMOM * nsub;  // <= 704 words (32 members)
+          // level 1 (the leaders): the records of their subgroup's members (<= 32: two words per thread), summed in member
+          // order (double) by wave 0's lanes j < NMOM and published for everyone
+          if (leader) {
+            const int nsub = sub_n(myk), nw = 2 * NMOM * nsub;  // <= 704 words (32 members)
             const int k2 = tid + NTHR;
-            const u64* pp[2] = {tid < nw ? slot(g + 8 * (tid / (2 * NMOM)), e4) + GW_P4 + tid % (2 * NMOM) : nullptr,
-                                k2 < nw ? slot(g + 8 * (k2 / (2 * NMOM)), e4) + GW_P4 + k2 % (2 * NMOM) : nullptr};
+            const u64* pp[2] = {tid < nw ? slot(sub_m(myk, tid / (2 * NMOM)), e4) + GW_P4 + tid % (2 * NMOM) : nullptr,
+                                k2 < nw ? slot(sub_m(myk, k2 / (2 * NMOM)), e4) + GW_P4 + k2 % (2 * NMOM) : nullptr};
             unsigned v[2];
             gpoll<2>(pp, tag4, v, a);
             if (tid < nw) sm.gw[tid] = v[0];
@@ -1165,9 +1196,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             }
             __syncthreads();  // the leader's words read before the leaders' partials land in sm.gw
           }
-          // level 2 (everyone): the 8 leaders' partial records
-          const int nw = 2 * NMOM * 8;
-          const u64* pp[1] = {tid < nw ? slot(tid / (2 * NMOM), e4) + GW_SUB4 + tid % (2 * NMOM) : nullptr};
+          // level 2 (everyone): the leaders' partial records
+          const int nw = 2 * NMOM * nlead;
+          const u64* pp[1] = {tid < nw ? slot(lead_m(tid / (2 * NMOM)), e4) + GW_SUB4 + tid % (2 * NMOM) : nullptr};
           unsigned v[1];
           gpoll<1>(pp, tag4, v, a);
           if (tid < nw) sm.gw[tid] = v[0];
@@ -1203,7 +1234,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // lane j < NMOM of every wave sums moment j over the members (one LDS load per member per wave),
         // then the 11 sums become wave-uniform by readlane
         const double* gd = reinterpret_cast<const double*>(sm.gw);
-        const double sj = seq_sum_lds(gd + (lane < NMOM ? lane : 0), NMOM, tree ? 8 : G);  // members, or the 8
+        const double sj = seq_sum_lds(gd + (lane < NMOM ? lane : 0), NMOM, tree ? nlead : G);  // members, or the 8
                                                                                               // leaders' partials
         double ms[NMOM];
 #pragma unroll

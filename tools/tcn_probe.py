@@ -25,6 +25,8 @@ def main(path):
     raw = np.fromfile(path, dtype=np.int64)
     grid, nblk, G, T = (int(v) for v in raw[:4])
     full = raw[4:4 + grid * nblk * 16].astype(np.float64).reshape(grid, nblk, 16) / 100.0  # us
+    keep = full[:, 0, 0] > 0  # (XCD-run launches: the blocks past a group's last member exit at once, no stamps)
+    full = full[keep]
     st = full[:, :, :13]
     ok = (st > 0).all(axis=2)
     d = np.diff(st, axis=2)  # [grid, nblk, 12]
@@ -57,7 +59,7 @@ def main(path):
     # per-wave phase durations (which waves a barrier waits for)
     n0 = grid * nblk * 16
     if raw.size >= 4 + 9 * n0:
-        W = raw[4 + n0: 4 + 9 * n0].astype(np.float64).reshape(grid, nblk, 16, 8) / 100.0
+        W = raw[4 + n0: 4 + 9 * n0].astype(np.float64).reshape(grid, nblk, 16, 8)[keep] / 100.0
         Ws = W[:, 1:, :13, :]
         if (Ws > 0).all():
             print("  per-wave: phase                 spread-at-end  per-wave median durations w0..w7 (us)")
