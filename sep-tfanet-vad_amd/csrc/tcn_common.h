@@ -3,6 +3,8 @@
 // flag", cdna_hip_programming.md Guideline 16 R2) with bounded polls, DPP lane reductions and the fp16 hi/lo
 // operand split.
 #pragma once
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace sepvad {
@@ -336,6 +338,78 @@ __device__ __forceinline__ float half_total(float v) {
   v += dpp_f<0x114>(v);
   v += dpp_f<0x118>(v);
   v += dpp_f<0x142>(v);
+  return v;
+}
+// Lane exchanges of the recursive-halving reductions (spectral.hip k_vad1): swap lanes L <-> L ^ 16 (v_permlane16_swap)
+// or L <-> L ^ 32 (v_permlane32_swap) between two registers. Inline asm: this hipcc's builtin pair result came back as the
+// same register twice (tools/probe_src/halving.hip); "s_nop 1" covers the VALU-write -> permlane hazard.
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+// Reduce-scatter of 16 values per lane over each 32-lane half of the wave: returns, in lane L, the sum over the 32
+// lanes of L's half of value (L & 31) >> 1 (lanes 2k and 2k + 1 both hold value k). Recursive halving (one
+// v_permlane16_swap level, DPP row_mirror / row_half_mirror / quad_perm levels, a final pair add): 8 swaps + 8 + 4 x 3 +
+// 2 x 3 + 3 + 1 VALU instead of 16 DPP chains of 5 (half_total). A fixed tree: deterministic.
+__device__ __forceinline__ float rs16_half(float (&x)[16], int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = x[j], b = x[j + 8];
+    swap16(a, b);  // bit 4 clear: keeps values 0..7 (own + partner's), set: 8..15
+    x[j] = a + b;
+  }
+  auto level = [&](auto CTRL, int msk, int n) {
+    constexpr int C = decltype(CTRL)::value;
+    const bool hi = (lane & msk) != 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < n / 2) {
+        const float send = hi ? x[j] : x[j + n / 2];
+        const float keep = hi ? x[j + n / 2] : x[j];
+        x[j] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), C, 0xf, 0xf, false));
+      }
+    }
+  };
+  level(std::integral_constant<int, 0x140>{}, 8, 8);  // row_mirror: lane i <-> 15 - i
+  level(std::integral_constant<int, 0x141>{}, 4, 4);  // row_half_mirror: i <-> 7 - i
+  level(std::integral_constant<int, 0x4e>{}, 2, 2);   // quad_perm [2,3,0,1]
+  return x[0] + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[0]), 0xb1, 0xf, 0xf, false));
+}
+// Reduce-scatter of 16 values per lane over all 64 lanes: returns, in lane L, the wave sum of value L >> 2 (the four
+// lanes of a quad hold the same sum). Levels: v_permlane32_swap, v_permlane16_swap, DPP row_mirror, row_half_mirror,
+// then two quad adds: 8 + 8 + 4 + 4 + 2 x 3 + 3 + 2 VALU instead of 16 chains of 6 DPP adds (half_total + row_bcast).
+__device__ __forceinline__ float rs16_wave(float (&x)[16], int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = x[j], b = x[j + 8];
+    swap32(a, b);  // lane bit 5 clear: keeps values 0..7, set: 8..15
+    x[j] = a + b;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = x[j], b = x[j + 4];
+    swap16(a, b);  // lane bit 4
+    x[j] = a + b;
+  }
+  auto level = [&](auto CTRL, int msk, int n) {
+    constexpr int C = decltype(CTRL)::value;
+    const bool hi = (lane & msk) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j < n / 2) {
+        const float send = hi ? x[j] : x[j + n / 2];
+        const float keep = hi ? x[j + n / 2] : x[j];
+        x[j] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), C, 0xf, 0xf, false));
+      }
+    }
+  };
+  level(std::integral_constant<int, 0x140>{}, 8, 4);  // row_mirror (lane bit 3)
+  level(std::integral_constant<int, 0x141>{}, 4, 2);  // row_half_mirror (lane bit 2)
+  float v = x[0];
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4e, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xb1, 0xf, 0xf, false));
   return v;
 }
 // Sum over the 64 lanes (+ row_bcast:31), returned wave-uniform (lane 63).

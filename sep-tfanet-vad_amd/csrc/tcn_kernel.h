@@ -56,6 +56,21 @@ namespace sepvad {
 // the GEMM waits for them): k_tcn -2.4 % shader cycles at cfg 2, bitwise equal (profiles/r05_prio/). 0 = round 4.
 #define TCN_PRIO 1
 #endif
+#ifndef TCN_FULLM
+// 1 (round 6): row loops without the frame masks where a workgroup's frames are all inside [0, T) (a second copy of
+// each loop, taken by a uniform branch); bitwise neutral; with it the two-slice kernels compile without spills
+#define TCN_FULLM 1
+#endif
+#ifndef TCN_BSRED
+// 1 (round 6): block_sums of more than 4 values (the moment record): reduce-scatters (rs16_wave) instead of DPP chains
+#define TCN_BSRED 1
+#endif
+#ifndef TCN_RSRED
+// 1 (round 6): row / frame sums: one reduce-scatter over the 32-lane halves (rs16_half) instead of 16 DPP chains of 5
+// (the removal probe TCN_DIAG=3 put those chains at 2.9 % of k_tcn's cycles); with TCN_BSRED and TCN_FULLM cfg 2 +3 %,
+// cfg 5 +7.8 % (profiles/r06w2/)
+#define TCN_RSRED 1
+#endif
 #ifndef TCN_WPIPE
 // 1 (round 6): the byte lo plane's widening one K step ahead (wave_gemm): -0.2 % k_tcn cycles at cfg 2, bitwise equal
 // (profiles/r06a/cyc.txt)
@@ -83,7 +98,8 @@ constexpr int LDDF = HID + 4;
 #endif
 constexpr int PD = TCN_PD;        // weight K steps in flight per wave
 #ifndef TCN_DIAG
-#define TCN_DIAG 0   // diagnostics only (wrong results): 1 = GEMM ring refills skipped, 2 = GEMM MFMAs skipped
+#define TCN_DIAG 0   // diagnostics only (wrong results): 1 = GEMM ring refills skipped, 2 = GEMM MFMAs skipped,
+                     // 3 = the frame sums' DPP reductions skipped (VALU-removal probe)
 #endif
 #ifndef TCN_AD
 #define TCN_AD 1     // GEMM A-fragment LDS reads issued this many K steps ahead (2: no gain, profiles/r03h_ab_*)
@@ -413,6 +429,18 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   // tid: the caller's recomputed thread id (tcn_common.h fresh_tid), so no value derived from threadIdx.x stays live
   // across the blocks (at 256 VGPRs hipcc spills such values to scratch and reloads them here behind vmcnt(0))
   const int w = tid >> 6;
+  if constexpr (TCN_BSRED && NV > 4) {
+    // wave totals by reduce-scatters of 16 values (rs16_wave: quad k of the wave holds value k), groups of 16
+#pragma unroll
+    for (int g0 = 0; g0 < NV; g0 += 16) {
+      float x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = g0 + j < NV ? v[g0 + j] : 0.f;
+      const float tv = rs16_wave(x, tid & 63);
+      const int j = g0 + ((tid & 63) >> 2);
+      if ((tid & 3) == 0 && j < NV) lds[j * 8 + w] = tv;
+    }
+  } else {
   float t[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {  // independent DPP chains (interleaved by the scheduler); lane 63 = total
@@ -422,6 +450,7 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* lds, double* o
   if ((tid & 63) == 63) {  // one branch for all NV stores
 #pragma unroll
     for (int j = 0; j < NV; ++j) lds[j * 8 + w] = t[j];
+  }
   }
   __syncthreads();
   if (tid < NV) {
@@ -670,6 +699,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       if (TP_ON && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
         a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
       const __half* wb = a.wfrag + (size_t)bi * WL::BLOCK;
+      // TCN_FULLM: every frame of this workgroup inside [0, T) (fullm), and every frame its depthwise conv reads (fulld):
+      // the frame-mask multiplies of the row loops compile away (a second copy of each loop; the masks are 1 there)
+      const bool fullm = TCN_FULLM && t0 + FW <= T, fulld = TCN_FULLM && t0 >= 4 && t0 + FW + 4 <= T;
       const int li = bi % a.layer;
       const int dil = li == 0 ? 1 : (li % 4 + 1);   // model/model.py:285-295 (as api.hip packs it)
       const float* pm = sm.prm;
@@ -711,7 +743,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const float ws = ws1, bias = b1;  // block_sums' barrier below makes the blob visible to later phases
         float st[2 * NSL];
         // packed fp32 over row pairs (r, r+1) = frames (tl, tl+1); per slice its own sums (member statistics)
-        {
+        auto epi_rows = [&](auto FULLC) {
+          constexpr bool FULL = decltype(FULLC)::value;
           const float a1m1 = a1 - 1.f;
 #pragma unroll
           for (int sl = 0; sl < NSL; ++sl) {
@@ -720,7 +753,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             for (int r = 0; r < 16; r += 2) {
               const int tl = trow(16 * sl + r);
               const f32x2 z = __builtin_elementwise_fma(f32x2{acc[sl][r], acc[sl][r + 1]}, f32x2{ws, ws}, f32x2{bias, bias});
-              const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+              const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
               const f32x2 v = prelu2(z, a1m1) * vm;
               sm.H[(tl + 4) * CH + m] = v.x;
               sm.H[(tl + 5) * CH + m] = v.y;
@@ -738,7 +771,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             st[2 * sl] = s0.x + s0.y;
             st[2 * sl + 1] = q0.x + q0.y;
           }
-        }
+        };
+        if (fullm) epi_rows(std::true_type{});
+        else epi_rows(std::false_type{});
         if (TCN_SUB == 2) TPROBE(13);
         block_sums<2 * NSL>(st, sm.red, sm.dred, tid);  // barrier inside: H complete
         if (TCN_SUB == 2) TPROBE(14);
@@ -806,14 +841,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const float a2m1 = a2 - 1.f;
         // rows fr0-D .. fr0+7+D of the pair once into registers (GN1 applied, zero outside [0, T)); H holds rows
         // -4..FW+3, so every load is in bounds and issued unconditionally
-        auto rows = [&](auto DC) {
+        auto rows = [&](auto DC, auto FULLC) {
           constexpr int D = decltype(DC)::value;
+          constexpr bool FULL = decltype(FULLC)::value;
           const float* hb = lds_base(sm.H + (fr0 - D + 4) * CH + c2);
           f32x2 hv[FR / 4 + 2 * D];
 #pragma unroll
           for (int i = 0; i < FR / 4 + 2 * D; ++i) {
             const int t = t0 + fr0 - D + i;
-            const float vm = (t >= 0 && t < T) ? 1.f : 0.f;  // mask multiply (a select sinks each load into a branch)
+            const float vm = FULL || (t >= 0 && t < T) ? 1.f : 0.f;  // mask multiply (a select sinks each load into a branch)
             hv[i] = __builtin_elementwise_fma(*reinterpret_cast<const f32x2*>(hb + i * CH), sc2, sh2) * vm;
           }
 #pragma unroll
@@ -822,7 +858,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             for (int e = 0; e < RPI; ++e)  // res_out ring entries RPI i .. RPI i + RPI - 1
               prefetch_w1<PRE, RD, LQ>(w2h, w2l, voff2, voff2l, rh, rl, RPI * i + e, sb);
             const int tl = fr0 + i;
-            const float vo = t0 + tl < T ? 1.f : 0.f;
+            const float vo = FULL || t0 + tl < T ? 1.f : 0.f;
             f32x2 y[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -837,12 +873,20 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
         };
         static_assert(RD == RPI * FR / 4, "RPI ring entries per frame of the packed depthwise conv");
-        switch (dil) {
-          case 1: rows(std::integral_constant<int, 1>{}); break;
-          case 2: rows(std::integral_constant<int, 2>{}); break;
-          case 3: rows(std::integral_constant<int, 3>{}); break;
-          default: rows(std::integral_constant<int, 4>{}); break;
-        }
+        auto rows_d = [&](auto FULLC) {
+#ifdef TCN_CENSUS_DIL  // static census builds only (tools/isa_phases.py): one dilation's code path, no switch
+          rows(std::integral_constant<int, TCN_CENSUS_DIL>{}, FULLC);
+          if (false)
+#endif
+          switch (dil) {
+            case 1: rows(std::integral_constant<int, 1>{}, FULLC); break;
+            case 2: rows(std::integral_constant<int, 2>{}, FULLC); break;
+            case 3: rows(std::integral_constant<int, 3>{}, FULLC); break;
+            default: rows(std::integral_constant<int, 4>{}, FULLC); break;
+          }
+        };
+        if (fulld) rows_d(std::true_type{});
+        else rows_d(std::false_type{});
       };
       {
         if (!LG) {
@@ -952,16 +996,36 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int sl = 0; sl < NSL; ++sl) {
             float rsum = 0.f, csr[16];
+            auto rsum_of = [&](auto FULLC) {
+              constexpr bool FULL = decltype(FULLC)::value;
+              float rs = 0.f;
+#pragma unroll
+              for (int r = 0; r < 16; ++r) rs += FULL || t0 + trow(16 * sl + r) < T ? acc[sl][r] : 0.f;
+              return rs;
+            };
+            rsum = fullm ? rsum_of(std::true_type{}) : rsum_of(std::false_type{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              rsum += t0 + trow(16 * sl + r) < T ? acc[sl][r] : 0.f;
-              csr[r] = half_total(ws * acc[sl][r]);  // ws-weighted sum over the wave's 32 channels (lanes 31 / 63)
+              if constexpr (TCN_RSRED) csr[r] = ws * acc[sl][r];
+              else
+              csr[r] = TCN_DIAG == 3 ? ws * acc[sl][r]  // (diagnostics: the 80 DPP adds per wave removed, wrong sums)
+                                     : half_total(ws * acc[sl][r]);  // ws-weighted sum over the wave's 32 channels (lanes 31 / 63)
             }
+            if constexpr (TCN_RSRED) {
+              // ws-weighted sums over the wave's 32 channels of each frame by one reduce-scatter (lane L: row (L & 31) / 2
+              // of its half), stored by the even lanes
+              const float cv = rs16_half(csr, lane);
+              if ((lane & 1) == 0) sm.cs[trow(16 * sl + ((lane & 31) >> 1))][wave] = cv;
+              float ro = rsum;
+              swap32(rsum, ro);  // (ro: the other half's frames; a + b == b + a, the bits of the __shfl_xor form)
+              rsum += ro;
+            } else {
             if ((lane & 31) == 31) {
 #pragma unroll
               for (int r = 0; r < 16; ++r) sm.cs[trow(16 * sl + r)][wave] = csr[r];
             }
             rsum += __shfl_xor(rsum, 32);
+            }
             if (hl == 0) gputf(slot(m0 + sl, e3) + GW_ROW + m, tag3, rsum, tree ? sl2 : l2);
           }
         }
@@ -1141,6 +1205,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // over its 16 rows of the slice first, then the channel weights once
         const float ga = LM == LD_RECURSIVE ? pm[PB_LNAG + m] : 0.f, be = LM == LD_RECURSIVE ? pm[PB_LNAB + m] : 0.f;
         float mo[NSL * NMOM];
+        auto mom_rows = [&](auto FULLC) {
+        constexpr bool FULL = decltype(FULLC)::value;
 #pragma unroll
         for (int sl = 0; sl < NSL; ++sl) {
           float so = 0.f, soo = 0.f, su = 0.f, suu = 0.f, sou = 0.f;
@@ -1149,7 +1215,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               const int tl = trow(16 * sl + r);
-              const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};  // masked, not branched
+              const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};  // masked, not branched
               const f32x2 rp = vm * f32x2{rv[sl][r], rv[sl][r + 1]};
               if constexpr (LM == LD_RECURSIVE) {
                 const f32x2 ov = vm * f32x2{o[16 * sl + r], o[16 * sl + r + 1]}, uv = ov + rp;
@@ -1170,6 +1236,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             ms[8] = ga * be * su; ms[9] = ga * ga * suu; ms[10] = ga * ga * su;
           }
         }
+        };
+        if (fullm) mom_rows(std::true_type{});
+        else mom_rows(std::false_type{});
         block_sums<NSL * NMOM>(mo, sm.red, sm.dred, tid);
       TPROBE(10);
         // ---- P4 words: the moment record (11 doubles) of each member; consume every member's ----
@@ -1264,6 +1333,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
+        auto xup_rows = [&](auto FULLC) {
+        constexpr bool FULL = decltype(FULLC)::value;
 #pragma unroll
         for (int r = 0; r < 16 * NSL; r += 2) {
           const int pr = r / 2;  // row pair: the ring entries are spread over the first 8 (one slice) or all 16 pairs
@@ -1274,12 +1345,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = trow(r);
           const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r >> 4][r & 15], rv[r >> 4][(r & 15) + 1]},
                                            kc);  // rv gated above
-          const f32x2 vm = {t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+          const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
           const f32x2 ov = x * vm;
           o[r] = ov.x; o[r + 1] = ov.y;
           if (TCN_XPK) split_store_rows_pk<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn, (lane & 1) != 0);
           else split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn);
         }
+        };
+        if (fullm) xup_rows(std::true_type{});
+        else xup_rows(std::false_type{});
       }
       __syncthreads();
       TPROBE(12);

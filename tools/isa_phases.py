@@ -9,9 +9,10 @@ import sys
 sys.path.insert(0, __file__.rsplit('/', 1)[0])
 from isa_stats import body_of, classify  # noqa: E402
 
-NAMES = {0: "block start", 1: "conv1d GEMM", 2: "epilogue+GN1+P1 publish", 3: "P1 wait", 4: "dwconv(+GN2)",
-         5: "res_out GEMM", 6: "rowsum/colsum", 7: "P3 publish", 8: "P3 wait + GN2 fold", 9: "gates",
-         10: "moments", 11: "P4 wait", 13: "kc", 14: "prefetch setup", 12: "x' update"}
+# the phase that STARTS at each stamp (TPROBE k in tcn_kernel.h), i.e. the code placed between stamp k and the next
+NAMES = {0: "conv1d GEMM", 1: "epilogue+GN1 sums", 2: "P1 publish/poll/halo", 3: "dwconv+GN2 sums", 4: "res_out GEMM",
+         5: "row/frame sums", 6: "P3 publish", 7: "P3 poll+GN2 fold", 8: "gates", 9: "moment record",
+         10: "P4 publish/poll", 11: "GN_a/GN_b finish", 13: "(after the loop: head)", 14: "x' update", 12: "loop end"}
 
 
 def main(path, key):
