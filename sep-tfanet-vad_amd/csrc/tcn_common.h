@@ -211,6 +211,20 @@ __device__ __forceinline__ void split_store2(_Float16* hi, _Float16* lo, int idx
 
 // ---- packed fp32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two channels per instruction) ----
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+#ifndef TCN_MIX
+#define TCN_MIX 1  // round 6: lo parts by v_fma_mix (bitwise equal, -0.5 % k_tcn cycles, profiles/r06mix/)
+#endif
+// The fp16 lo parts of a pair, (f16)(v - (float)h) with hb = the pair's hi halves, as two v_fma_mix (hi read as f16,
+// the difference rounded to f16 once): v - h is exact in fp32 (h is v rounded to fp16), so the bits equal the
+// convert / subtract / convert form, in 2 instructions instead of 5. Inline asm (no builtin); the closing s_nop 1 covers
+// a DPP or permlane reader of the result (split_store_rows_pk).
+__device__ __forceinline__ unsigned lo_pair_mix(f32x2 v, unsigned hb) {
+  unsigned r;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1"
+      : "=&v"(r) : "v"(v.x), "v"(v.y), "v"(hb));
+  return r;
+}
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
@@ -235,9 +249,14 @@ __device__ __forceinline__ void store_d4(_Float16* hi, _Float16* lo, f32x2 y0, f
   const f32x2 a = {y0.x, y1.x}, b = {y0.y, y1.y};  // hidden 2c, 2c+1 | 2c+2, 2c+3
   if constexpr (PRE == PREC_F16X3) {
     const f16x2v ha = __builtin_convertvector(a, f16x2v), hb = __builtin_convertvector(b, f16x2v);
+    *reinterpret_cast<u32x2v*>(hi) = u32x2v{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+    if constexpr (TCN_MIX) {
+      *reinterpret_cast<u32x2v*>(lo) = u32x2v{lo_pair_mix(a, __builtin_bit_cast(unsigned, ha)),
+                                              lo_pair_mix(b, __builtin_bit_cast(unsigned, hb))};
+      return;
+    }
     const f16x2v la = __builtin_convertvector(a - __builtin_convertvector(ha, f32x2), f16x2v);
     const f16x2v lb = __builtin_convertvector(b - __builtin_convertvector(hb, f32x2), f16x2v);
-    *reinterpret_cast<u32x2v*>(hi) = u32x2v{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
     *reinterpret_cast<u32x2v*>(lo) = u32x2v{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
   } else if constexpr (PRE == PREC_F16) {
     const f16x2v ha = __builtin_convertvector(a, f16x2v), hb = __builtin_convertvector(b, f16x2v);
@@ -283,8 +302,12 @@ __device__ __forceinline__ void split_store_rows_pk(_Float16* hi, _Float16* lo, 
   };
   if constexpr (PRE == PREC_F16X3) {
     const f16x2v h = __builtin_convertvector(v, f16x2v);
-    const f16x2v l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2v);
     put(hi, __builtin_bit_cast(unsigned, h));
+    if constexpr (TCN_MIX) {
+      put(lo, lo_pair_mix(v, __builtin_bit_cast(unsigned, h)));
+      return;
+    }
+    const f16x2v l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2v);
     put(lo, __builtin_bit_cast(unsigned, l));
   } else if constexpr (PRE == PREC_F16) {
     put(hi, __builtin_bit_cast(unsigned, __builtin_convertvector(v, f16x2v)));
