@@ -699,9 +699,18 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       if (TP_ON && tid == 0 && u == grp && a.nblk > 5 && (bi == 0 || bi == 2))
         a.probe[((size_t)blockIdx.x * a.nblk + 4 + bi / 2) * 16 + 15] = __builtin_amdgcn_s_memtime();
       const __half* wb = a.wfrag + (size_t)bi * WL::BLOCK;
-      // TCN_FULLM: every frame of this workgroup inside [0, T) (fullm), and every frame its depthwise conv reads (fulld):
-      // the frame-mask multiplies of the row loops compile away (a second copy of each loop; the masks are 1 there)
-      const bool fullm = TCN_FULLM && t0 + FW <= T, fulld = TCN_FULLM && t0 >= 4 && t0 + FW + 4 <= T;
+      // TCN_FULLM: the frame masks of the row loops (rows r, r + 1 of a lane's tile rows: pair p = r / 2 of 8 NSL) only
+      // where a frame can be outside [0, T): none when every frame of the workgroup is inside (mpw = 0), the last two
+      // pairs when only its last 8 frames can be out (mpw = 2: the other pairs hold frames <= FW - 9; T mod 32 >= 24,
+      // e.g. T = 126, 188, 251), else all (a copy of each loop per case; the masks are 1 where skipped). The partial last
+      // member set every group's pace (the masked loops: cfg 2 138.1k vs 145.8k utt/s, profiles/r06mp/). The depthwise
+      // conv decides per wave (its 8 rows + halo).
+      const int mpw = !TCN_FULLM ? 8 * NSL : (t0 + FW <= T ? 0 : (t0 + FW - 8 <= T ? 2 : 8 * NSL));
+      auto by_mp = [&](auto&& f) {
+        if (mpw == 0) f(std::integral_constant<int, 0>{});
+        else if (mpw == 2) f(std::integral_constant<int, 2>{});
+        else f(std::integral_constant<int, 8 * NSL>{});
+      };
       const int li = bi % a.layer;
       const int dil = li == 0 ? 1 : (li % 4 + 1);   // model/model.py:285-295 (as api.hip packs it)
       const float* pm = sm.prm;
@@ -743,8 +752,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         const float ws = ws1, bias = b1;  // block_sums' barrier below makes the blob visible to later phases
         float st[2 * NSL];
         // packed fp32 over row pairs (r, r+1) = frames (tl, tl+1); per slice its own sums (member statistics)
-        auto epi_rows = [&](auto FULLC) {
-          constexpr bool FULL = decltype(FULLC)::value;
+        auto epi_rows = [&](auto MPC) {
+          constexpr int MP = decltype(MPC)::value;
           const float a1m1 = a1 - 1.f;
 #pragma unroll
           for (int sl = 0; sl < NSL; ++sl) {
@@ -753,7 +762,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             for (int r = 0; r < 16; r += 2) {
               const int tl = trow(16 * sl + r);
               const f32x2 z = __builtin_elementwise_fma(f32x2{acc[sl][r], acc[sl][r + 1]}, f32x2{ws, ws}, f32x2{bias, bias});
-              const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+              const f32x2 vm = 8 * sl + r / 2 < 8 * NSL - MP ? f32x2{1.f, 1.f}
+                                                             : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
               const f32x2 v = prelu2(z, a1m1) * vm;
               sm.H[(tl + 4) * CH + m] = v.x;
               sm.H[(tl + 5) * CH + m] = v.y;
@@ -772,8 +782,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             st[2 * sl + 1] = q0.x + q0.y;
           }
         };
-        if (fullm) epi_rows(std::true_type{});
-        else epi_rows(std::false_type{});
+        by_mp(epi_rows);
         if (TCN_SUB == 2) TPROBE(13);
         block_sums<2 * NSL>(st, sm.red, sm.dred, tid);  // barrier inside: H complete
         if (TCN_SUB == 2) TPROBE(14);
@@ -885,7 +894,9 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
             default: rows(std::integral_constant<int, 4>{}, FULLC); break;
           }
         };
-        if (fulld) rows_d(std::true_type{});
+        // (per wave: the thread's 8 rows fr0 .. fr0 + 7 and their halo, wave-uniform in both layouts)
+        const bool fullw = __builtin_amdgcn_readfirstlane((int)(TCN_FULLM && t0 + fr0 - 4 >= 0 && t0 + fr0 + FR / 4 + 4 <= T)) != 0;
+        if (fullw) rows_d(std::true_type{});
         else rows_d(std::false_type{});
       };
       {
@@ -996,14 +1007,14 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
           for (int sl = 0; sl < NSL; ++sl) {
             float rsum = 0.f, csr[16];
-            auto rsum_of = [&](auto FULLC) {
-              constexpr bool FULL = decltype(FULLC)::value;
+            by_mp([&](auto MPC) {
+              constexpr int MP = decltype(MPC)::value;
               float rs = 0.f;
 #pragma unroll
-              for (int r = 0; r < 16; ++r) rs += FULL || t0 + trow(16 * sl + r) < T ? acc[sl][r] : 0.f;
-              return rs;
-            };
-            rsum = fullm ? rsum_of(std::true_type{}) : rsum_of(std::false_type{});
+              for (int r = 0; r < 16; ++r)
+                rs += 8 * sl + r / 2 < 8 * NSL - MP || t0 + trow(16 * sl + r) < T ? acc[sl][r] : 0.f;
+              rsum = rs;
+            });
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               if constexpr (TCN_RSRED) csr[r] = ws * acc[sl][r];
@@ -1205,8 +1216,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
         // over its 16 rows of the slice first, then the channel weights once
         const float ga = LM == LD_RECURSIVE ? pm[PB_LNAG + m] : 0.f, be = LM == LD_RECURSIVE ? pm[PB_LNAB + m] : 0.f;
         float mo[NSL * NMOM];
-        auto mom_rows = [&](auto FULLC) {
-        constexpr bool FULL = decltype(FULLC)::value;
+        auto mom_rows = [&](auto MPC) {
+        constexpr int MP = decltype(MPC)::value;
 #pragma unroll
         for (int sl = 0; sl < NSL; ++sl) {
           float so = 0.f, soo = 0.f, su = 0.f, suu = 0.f, sou = 0.f;
@@ -1215,7 +1226,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               const int tl = trow(16 * sl + r);
-              const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};  // masked, not branched
+              const f32x2 vm = 8 * sl + r / 2 < 8 * NSL - MP ? f32x2{1.f, 1.f}  // masked, not branched
+                                                             : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
               const f32x2 rp = vm * f32x2{rv[sl][r], rv[sl][r + 1]};
               if constexpr (LM == LD_RECURSIVE) {
                 const f32x2 ov = vm * f32x2{o[16 * sl + r], o[16 * sl + r + 1]}, uv = ov + rp;
@@ -1237,8 +1249,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
         }
         };
-        if (fullm) mom_rows(std::true_type{});
-        else mom_rows(std::false_type{});
+        by_mp(mom_rows);
         block_sums<NSL * NMOM>(mo, sm.red, sm.dred, tid);
       TPROBE(10);
         // ---- P4 words: the moment record (11 doubles) of each member; consume every member's ----
@@ -1333,8 +1344,8 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       // x' = next block input: o (registers) and the conv1d A operand (LDS, scaled by the next block's 2^-e)
       {
         const float sxn = pm[PB_SXN];
-        auto xup_rows = [&](auto FULLC) {
-        constexpr bool FULL = decltype(FULLC)::value;
+        auto xup_rows = [&](auto MPC) {
+        constexpr int MP = decltype(MPC)::value;
 #pragma unroll
         for (int r = 0; r < 16 * NSL; r += 2) {
           const int pr = r / 2;  // row pair: the ring entries are spread over the first 8 (one slice) or all 16 pairs
@@ -1345,15 +1356,15 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           const int tl = trow(r);
           const f32x2 x = resid_apply2<LM>(f32x2{o[r], o[r + 1]}, f32x2{rv[r >> 4][r & 15], rv[r >> 4][(r & 15) + 1]},
                                            kc);  // rv gated above
-          const f32x2 vm = FULL ? f32x2{1.f, 1.f} : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
+          const f32x2 vm = r / 2 < 8 * NSL - MP ? f32x2{1.f, 1.f}
+                                                : f32x2{t0 + tl < T ? 1.f : 0.f, t0 + tl + 1 < T ? 1.f : 0.f};
           const f32x2 ov = x * vm;
           o[r] = ov.x; o[r + 1] = ov.y;
           if (TCN_XPK) split_store_rows_pk<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn, (lane & 1) != 0);
           else split_store_rows<PRE>(sm.Ahi, sm.Alo, tl * LDXE + m, LDXE, ov * sxn);
         }
         };
-        if (fullm) xup_rows(std::true_type{});
-        else xup_rows(std::false_type{});
+        by_mp(xup_rows);
       }
       __syncthreads();
       TPROBE(12);
