@@ -61,6 +61,9 @@ namespace sepvad {
 // each loop, taken by a uniform branch); bitwise neutral; with it the two-slice kernels compile without spills
 #define TCN_FULLM 1
 #endif
+#ifndef TCN_FULLDW
+#define TCN_FULLDW 1  // TCN_FULLM for the depthwise conv too (a second copy of its 4 dilation variants)
+#endif
 #ifndef TCN_BSRED
 // 1 (round 6): block_sums of more than 4 values (the moment record): reduce-scatters (rs16_wave) instead of DPP chains
 #define TCN_BSRED 1
@@ -895,7 +898,7 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
           }
         };
         // (per wave: the thread's 8 rows fr0 .. fr0 + 7 and their halo, wave-uniform in both layouts)
-        const bool fullw = __builtin_amdgcn_readfirstlane((int)(TCN_FULLM && t0 + fr0 - 4 >= 0 && t0 + fr0 + FR / 4 + 4 <= T)) != 0;
+        const bool fullw = TCN_FULLDW && __builtin_amdgcn_readfirstlane((int)(TCN_FULLM && t0 + fr0 - 4 >= 0 && t0 + fr0 + FR / 4 + 4 <= T)) != 0;
         if (fullw) rows_d(std::true_type{});
         else rows_d(std::false_type{});
       };
