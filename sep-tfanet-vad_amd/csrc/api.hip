@@ -1455,10 +1455,12 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from the output head's tap products (k_vad_feat,
   // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
-  // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, the same arithmetic; measured
-  // equal speed: 114.2k vs 114.4k utt/s, profiles/r02av_ab_vadfeat.txt — the in-kernel BN_1 sums lengthen
-  // k_istft_pair by what the launch saves), default 1: k_vad_feat
-  const bool vad_taps_in_istft = vad_in_head && !env_int("SEPVAD_VAD_FEAT", 1);
+  // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, k_vad_feat<4>'s items and order:
+  // the same bits), 1: k_vad_feat. Default: inside k_istft_pair for T <= 256, where every k_istft_pair workgroup's
+  // whole-utterance BN_1 sums are 2 items per thread (cfg 2: +0.4 %, 152.4k vs 151.9k utt/s interleaved,
+  // profiles/r06pv/vadfeat_lines.txt; round 2 had measured equal, profiles/r02av_ab_vadfeat.txt); longer utterances
+  // keep k_vad_feat (each of the T / 11 workgroups would sum all 4 T items).
+  const bool vad_taps_in_istft = vad_in_head && !env_int("SEPVAD_VAD_FEAT", T > 256 ? 1 : 0);
   if (vad_in_head && !vad_taps_in_istft) {
     VadFeatArgs vf{};
     vf.B = B; vf.T = T; vf.Tp = Tp; vf.vP = w.vP;

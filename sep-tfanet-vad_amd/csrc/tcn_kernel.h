@@ -84,6 +84,16 @@ namespace sepvad {
 // whose vmcnt wait then also waited for the block-parameter loads): -0.5 % cycles, with TCN_WPIPE -0.7 %, bitwise equal
 #define TCN_A1V 1
 #endif
+#ifndef TCN_PP
+// 1 (round 6, measured, not kept): one-slice depthwise conv + res_out GEMM as a wave-role ping-pong. Waves 4-7 (s_setprio
+// 1) compute the first K half of d (input channels 0..127) and start their res_out MFMAs on it while waves 0-3 compute the
+// second half on the same SIMDs; waves 0-3 then run their whole K, waves 4-7 the second half. Hand-over by two LDS
+// counters (no workgroup barrier); the same d, the same K order, the GN2 wave totals in the plain mapping's order: the
+// same bits (digests equal at cfg 2 and cfg 5). Waves 0-3's half of d slows from 2.16 to 2.44 us beside the MFMAs and
+// their 32 K steps still take 4.0 us, so the pair of phases shrinks by 0.2 us per block only, while the kernel spills 29
+// VGPRs around its prologue and head: k_tcn +2.4 % cycles at cfg 2 (profiles/r06pp/).
+#define TCN_PP 0
+#endif
 #ifndef TCN_SUB
 #define TCN_SUB 0    // probe sub-stamps 13/14: 0 in the x' update, 1 in the depthwise conv (diagnostics)
 #endif
@@ -140,6 +150,8 @@ struct TcnSmem {
   unsigned gw[GW_WORDS] __attribute__((aligned(8)));  // gathered statistic words (GN words, moment records)
   double dred[16];
   float prm[PB_SIZE];             // this block's parameter blob (PB_*)
+  float pps[16];                  // TCN_PP: the GN2 wave totals {sum [8], sumsq [8]}
+  unsigned ppc[2];                // TCN_PP: waves done with K half 0 / 1 of d (4 per block)
 };
 static_assert(offsetof(TcnSmem, Alo) == offsetof(TcnSmem, Ahi) + sizeof(TcnSmem::Ahi) &&
               16 * FR * HEAD_VAD_N * 4 <= sizeof(TcnSmem::H) && 4 * FR * 32 * 2 <= FR * (LDD - LDX) &&
@@ -256,7 +268,9 @@ __device__ __forceinline__ void wave_gemm_f32(f32x16v (&acc)[NT], const float* A
   for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
 }
 
-template <int NS, int LDA, int PRE, int RD = PD, int LQ = 0, int NT = 1, int KS0 = 0>
+// CONT: the ring keeps streaming past the last step (steps KS0 + NS .. KS0 + NS + RD - 1 in flight on return, for a
+// following call with KS0 + NS)
+template <int NS, int LDA, int PRE, int RD = PD, int LQ = 0, int NT = 1, int KS0 = 0, bool CONT = false>
 __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ahi, const _Float16* Alo,
                                           __amdgpu_buffer_rsrc_t wh, __amdgpu_buffer_rsrc_t wl, int voff, int voffl,
                                           u32x4v (&rh)[RD], u32x4v (&rl)[RD], int lane) {
@@ -353,7 +367,7 @@ __device__ __forceinline__ void wave_gemm(f32x16v (&acc)[NT], const _Float16* Ah
     for (int i = 0; i < RD; ++i) step(s0 + i, i, true);
   }
 #pragma unroll
-  for (int i = 0; i < RD; ++i) step(NS - RD + i, i, false);
+  for (int i = 0; i < RD; ++i) step(NS - RD + i, i, CONT);
   }
 }
 
@@ -541,6 +555,11 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
   // epoch 1: this workgroup's XCD id for each of its members (write-through), polled in the first utterance's prologue
   if (tid < NSL && grp < a.B)
     gput(slot(m0 + tid, 1), a.tag0 + 1, __builtin_amdgcn_s_getreg(6164) & 0xfu, false);  // hwreg(HW_REG_XCC_ID, 0, 4)
+  constexpr bool PP = TCN_PP && NSL == 1 && !F32;
+  unsigned ppn = 0;  // TCN_PP: blocks run by this workgroup (the LDS counters' target is 4 ppn)
+  if constexpr (PP) {
+    if (tid < 2) sm.ppc[tid] = 0u;  // (the prologue's barriers order this before every use)
+  }
   if (!a.tf_att) {  // no TF-attention: unit gates, so the gating multiply below is exact (two slices: not applied)
     if (tid < CH) sm.af[tid] = 1.f;
     if (tid < FW) sm.at[tid] = 1.f;
@@ -912,7 +931,30 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       }
       // ---- P2 words: GN2 partial sums (awaited after the res_out main loop) ----
       const unsigned e2 = ++ep, tag2 = a.tag0 + e2;
-      if constexpr (NSL == 1) {
+      // TCN_PP hand-over: wait until the 4 waves of K half hh have stored their d rows (LDS counter; s_sleep between reads)
+      auto pp_wait = [&](int hh) {
+        if constexpr (PP) {
+          while (__hip_atomic_load(&sm.ppc[hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * ppn)
+            __builtin_amdgcn_s_sleep(1);
+          asm volatile("" ::: "memory");
+        }
+      };
+      if constexpr (PP) {
+        // waves 4-7 (the s_setprio 1 waves: they win the VALU while both compute d) take K half 0 = input channels
+        // 0..127, waves 0-3 half 1; wave w's frames 8 (w & 3) .. + 7; vw = its wave in the plain mapping below
+        ++ppn;
+        const int hh = wave_s >= 4 ? 0 : 1, fq = wave_s & 3, vw = 2 * fq + hh;
+        f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+        dwconv(std::integral_constant<int, LDDE>{}, 2 * (64 * hh + lane), fq * (FR / 4), 0, 0, s0, s1);
+        // block_sums<2>'s wave totals (lane 63), at the plain mapping's wave index
+        float t0v = half_total(s0.x + s0.y), t1v = half_total(s1.x + s1.y);
+        t0v += dpp_f<0x143>(t0v);
+        t1v += dpp_f<0x143>(t1v);
+        if (lane == 63) { sm.pps[vw] = t0v; sm.pps[8 + vw] = t1v; }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's d rows and totals stored
+        if (lane == 0) __hip_atomic_fetch_add(&sm.ppc[hh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      TPROBE(4);
+      } else if constexpr (NSL == 1) {
         if (TCN_SUB == 1) TPROBE(13);
         f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
         // thread = input channels c2, c2+1 (hidden 2c2..2c2+3) x frames fr0..fr0+7
@@ -928,7 +970,25 @@ __global__ __launch_bounds__(NTHR) void k_tcn(TcnArgs a) {
       for (int sl = 0; sl < NSL; ++sl)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[sl][r] = 0.f;
-      if constexpr (NSL == 1) {
+      if constexpr (PP) {
+        if (wave_s >= 4) {  // K half 0 as soon as its d is complete, then half 1
+          pp_wait(0);
+          wave_gemm<NS2 / 2, LDDE, PRE, RD, LQ, 1, 0, true>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, voff2l, rh, rl, lane);
+          pp_wait(1);
+          wave_gemm<NS2 / 2, LDDE, PRE, RD, LQ, 1, NS2 / 2>(acc, plane_at<PRE>(sm.Ahi, HID / 2), plane_at<PRE>(sm.Alo, HID / 2),
+                                                           w2h, w2l, voff2, voff2l, rh, rl, lane);
+        } else {  // all of d, then the whole K; threads 0, 1 publish the GN2 words (block_sums<2>'s order and bits)
+          pp_wait(1);
+          pp_wait(0);
+          if (tid < 2) {
+            double t = 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t += sm.pps[tid * 8 + i];
+            gputd(slot(g, e2) + GW_STAT + 2 * tid, tag2, t, l2);
+          }
+          wave_gemm<NS2, LDDE, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, voff2l, rh, rl, lane);
+        }
+      } else if constexpr (NSL == 1) {
         wave_gemm<NS2, LDDE, PRE, RD, LQ>(acc, sm.Ahi, sm.Alo, w2h, w2l, voff2, voff2l, rh, rl, lane);
       } else {
         // two K halves of 256 hidden channels each (input channels 0..127, then 128..255 of the depthwise conv) through

@@ -406,6 +406,23 @@ def test_vad_taps_finished_in_istft(nets):
     assert np.abs(vg.cpu().numpy() - g["vad"]).max() <= VAD_PROB_TOL
 
 
+def test_vad_taps_in_istft_default_short_utterances(nets):
+    """T <= 256 defaults to the in-k_istft_pair VAD features (SEPVAD_VAD_FEAT unset); they take k_vad_feat<4>'s items
+    and summation order, so the outputs equal the k_vad_feat schedule's (SEPVAD_VAD_FEAT=1) bit for bit."""
+    import os
+    from sep_tfanet_vad_amd import synth
+    net = nets["with_vad"]
+    x = torch.from_numpy(synth.make_batch(9, 32000, 516)[0]).to(DEV)
+    a, va, ea, _ = _run(net, x, True)
+    os.environ["SEPVAD_VAD_FEAT"] = "1"
+    try:
+        b, vb, eb, _ = _run(net, x, True)
+    finally:
+        del os.environ["SEPVAD_VAD_FEAT"]
+    assert torch.equal(a, b) and torch.equal(va, vb)
+    assert (ea is None and eb is None) or torch.equal(ea, eb)
+
+
 def test_long_files_full_chip_groups(nets, state_dicts):
     """16 s files at B=8 (bench --workload long): 8 groups of 32 members fill the 256 CUs, each group on one
     XCD (the L2-resident hand-off protocol), at T = 1001 (two-pass moment polls, LDS GroupNorm finish)."""
