@@ -1455,8 +1455,8 @@ int enqueue_chunk(sepvad_model* h, StreamCtx* cx, const float* x, int ldx, int b
   // 5. VAD conv1_1 (model/model.py:424-427,434-436): finished from the output head's tap products (k_vad_feat,
   // BN_1-normalised features), or the whole conv on the masks (k_vad1 + records)
   const bool kw_on = kw && kw->enabled && c.final_vad;
-  // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, k_vad_feat<4>'s items and order:
-  // the same bits), 1: k_vad_feat. Default: inside k_istft_pair for T <= 256, where every k_istft_pair workgroup's
+  // SEPVAD_VAD_FEAT=0: the tap sums finished inside k_istft_pair (one launch fewer, k_vad_feat<4>'s items and order;
+  // the BN_1 affine rounds differently: VAD probabilities equal to fp32 rounding), 1: k_vad_feat. Default: inside k_istft_pair for T <= 256, where every k_istft_pair workgroup's
   // whole-utterance BN_1 sums are 2 items per thread (cfg 2: +0.4 %, 152.4k vs 151.9k utt/s interleaved,
   // profiles/r06pv/vadfeat_lines.txt; round 2 had measured equal, profiles/r02av_ab_vadfeat.txt); longer utterances
   // keep k_vad_feat (each of the T / 11 workgroups would sum all 4 T items).
