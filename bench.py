@@ -85,8 +85,8 @@ def tcn_bytes(B, T, precision="f16x3", wlo="f16"):
             + (24 * (256 * 256 + 256 * 512) + HEAD_ROWS_MFMA * 256) * wbytes)
 
 
-TA_FILE = "r05prof_pmc_ta_summary.txt"  # texture-path counters of k_tcn (tools/r05_profile.sh), cfg 2, f16x3, i8 lo
-CACHE_FILE = "r05prof_coexec_tcc_dram.txt"  # MFMA/VALU co-issue, L2 hit/miss and memory-side read counters
+TA_FILE = "r06prof_pmc_ta_summary.txt"  # texture-path counters of k_tcn (tools/r05_profile.sh), cfg 2, f16x3, i8 lo
+CACHE_FILE = "r06prof_coexec_tcc_dram.txt"  # MFMA/VALU co-issue, L2 hit/miss and memory-side read counters
 RING_FILE = "r02bi_ring_gemm.txt"       # GEMM-phase stream floor per CU (tools/probe_src/ring_gemm.hip)
 STREAM_FLOOR_GBPS = 103.2
 
@@ -154,7 +154,7 @@ def res_out_bytes(B, T):
     return B * Tp * 512 * 4 + B * Tp * 256 * 4 + 256 * 512 * 4
 
 
-STATS_FILE = "r05prof_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
+STATS_FILE = "r06prof_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline bench command (cfg 2, f16x3)
 TCN_KERNEL_PREFIX = "void sepvad::k_tcn<2, 1, false, 2, false, false, 1>"  # the dominant kernel's name in that file
 
 
@@ -173,7 +173,7 @@ def rocprof_avg_us(kernel_prefix):
 
 
 PMC_FILE = "r01h_pmc_res_out.json"       # multi-kernel schedule (res_out GEMM)
-PMC_FILE_FUSED = "r05prof_pmc_tcn.json"     # fused schedule (k_tcn)
+PMC_FILE_FUSED = "r06prof_pmc_tcn.json"     # fused schedule (k_tcn)
 PMC_WLO = "i8"                             # ... measured with this weight lo plane
 DEFAULT_SPLIT = 1
 # Default (timed steps, warmup steps) per workload: ~0.1 s of untimed load, then ~0.5 s timed. The shader clock ramps
