@@ -56,6 +56,9 @@ __device__ __forceinline__ double dword2(unsigned lo, unsigned hi) {
 #ifndef TCN_POLL_SERIAL
 #define TCN_POLL_SERIAL 0
 #endif
+#ifndef TCN_POLL_SLEEP
+#define TCN_POLL_SLEEP 1  // s_sleep between poll passes (units of 64 clocks; 0 = none)
+#endif
 // A bounded hand-off wait gave up: record this launch's tag0 in the device word and its host-mapped copy.
 __device__ __forceinline__ void giveup(const TcnArgs& a) {
   __hip_atomic_store(a.err, a.tag0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -97,7 +100,7 @@ __device__ __forceinline__ void gpollt(const u64* const (&p)[N], const unsigned 
       ok = ok && (p[k] == nullptr || (unsigned)(x[k] >> 32) == tag[k]);
     }
     if (ok) return;
-    __builtin_amdgcn_s_sleep(1);
+    if (TCN_POLL_SLEEP) __builtin_amdgcn_s_sleep(TCN_POLL_SLEEP);
     if ((++spins & 255u) == 0 &&
         (spins > a.spin_limit || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.tag0)) {
       if (spins > a.spin_limit) {  // diagnostics: the first timed-out wait of the launch {tag, workgroup, word}
